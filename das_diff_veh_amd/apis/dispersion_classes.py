@@ -1,0 +1,115 @@
+"""SurfaceWaveDispersion — drop-in for apis/dispersion_classes.py:9-65 of the reference.
+
+Per-pass dispersion image straight from a window ("naive": raw channel slice, :24-32; "smart":
+time + trajectory mutes on a copy first, :34-43), with the reference's stacking arithmetic.
+``batched_surface_wave_dispersion`` is the batched flavour-B path used by
+DispersionImagesFromWindows.get_images: all passes in one launch of each dispersion kernel, the
+per-class mean f-v image formed on device.
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+
+from ..modules.utils import Dispersion, disp_plan
+
+
+class SurfaceWaveDispersion:
+    def __init__(self, window, freqs=np.arange(0.8, 25, 0.1), vels=np.arange(200, 1200), method="naive", norm=True,
+                 **method_kwargs):
+        self.window = window
+        self.freqs = freqs
+        self.vels = vels
+        self.method = method
+        self.norm = norm
+        if method == "naive":
+            self._naive_disp(**method_kwargs)
+        else:
+            self._smart_disp(**method_kwargs)
+
+    def _naive_disp(self, start_x, end_x):
+        dist = end_x - start_x
+        window = self.window
+        dx = window.x_axis[1] - window.x_axis[0]
+        s = int(np.argmax(window.x_axis >= start_x))
+        nx = int(dist / dx)
+        self.disp = Dispersion(window.data[s:s + nx], dx, window.t_axis[1] - window.t_axis[0], freqs=self.freqs,
+                               vels=self.vels, norm=self.norm)
+
+    def _smart_disp(self, mute_along_time=True, time_alpha=0.3, mute_along_traj=True):
+        w = copy.deepcopy(self.window)
+        if mute_along_time and not getattr(w, "muted_along_time", False):
+            w.mute_along_time(alpha=time_alpha)
+        if mute_along_traj and not getattr(w, "muted_along_traj", False):
+            w.mute_along_traj()
+        dx = w.x_axis[1] - w.x_axis[0]
+        self.disp = Dispersion(w.data, dx, w.t_axis[1] - w.t_axis[0], freqs=self.freqs, vels=self.vels,
+                               norm=self.norm)
+
+    def save_to_npz(self, *args, **kwargs):
+        self.disp.save_to_npz(*args, **kwargs)
+
+    def plot_image(self, *args, **kwargs):
+        self.disp.plot_image(*args, **kwargs)
+
+    def __add__(self, other):
+        sum_ = copy.deepcopy(self)
+        sum_.disp = self.disp + other.disp
+        return sum_
+
+    def __radd__(self, other):
+        if other == 0:
+            return self
+        return self.__add__(other)
+
+    def __truediv__(self, other):
+        new_obj = copy.deepcopy(self)
+        new_obj.disp = self.disp / other
+        return new_obj
+
+    @classmethod
+    def _from_fv(cls, window, freqs, vels, method, norm, fv):
+        obj = cls.__new__(cls)
+        obj.window, obj.freqs, obj.vels, obj.method, obj.norm = window, freqs, vels, method, norm
+        obj.disp = Dispersion(None, None, None, freqs, vels, norm=norm, compute_fv=False)
+        obj.disp.fv_map = fv
+        return obj
+
+
+def batched_surface_wave_dispersion(windows, norm=False, freqs=np.arange(0.8, 25, 0.1), vels=np.arange(200, 1200),
+                                    method="naive", start_x=None, end_x=None, **kw):
+    """(images, avg_image) of ImagesFromWindows.get_images for image_cls=SurfaceWaveDispersion,
+    naive method: one launch per kernel for all windows of a shape."""
+    from ..device import to_device_f32
+    from ..disp import fk_grid, fv_from_fk
+    if method != "naive" or kw:
+        images = [SurfaceWaveDispersion(w, freqs=freqs, vels=vels, method=method, norm=norm,
+                                        **({} if method != "naive" else dict(start_x=start_x, end_x=end_x)), **kw)
+                  for w in windows]
+        avg = sum(images) / len(images)
+        return images, avg
+    groups = {}
+    for i, w in enumerate(windows):
+        dx = w.x_axis[1] - w.x_axis[0]
+        s = int(np.argmax(w.x_axis >= start_x))
+        nx = int((end_x - start_x) / dx)
+        key = (tuple(np.shape(w.data)), s, nx, float(dx), float(w.t_axis[1] - w.t_axis[0]))
+        groups.setdefault(key, []).append(i)
+    n = len(windows)
+    acc = None
+    per_pass = [None] * n
+    for (shape, s, nx, dx, dt), idx in groups.items():
+        data = to_device_f32([windows[i].data for i in idx])[:, s:s + nx, :]
+        plan = disp_plan(data.shape[1], data.shape[2], dx, dt, freqs, vels)
+        FK = fk_grid(data, plan, norm=norm)
+        fv = fv_from_fk(FK, plan)
+        host = fv.to("cpu").numpy()
+        for k, i in enumerate(idx):
+            per_pass[i] = host[k]
+        part = fv.sum(dim=0)
+        acc = part if acc is None else acc + part
+    images = [SurfaceWaveDispersion._from_fv(w, freqs, vels, method, norm, per_pass[i]) for i, w in enumerate(windows)]
+    avg_fv = (acc / n).to("cpu").numpy()
+    avg = SurfaceWaveDispersion._from_fv(windows[0], freqs, vels, method, norm, avg_fv)
+    return images, avg

@@ -1,0 +1,92 @@
+"""Per-class imaging orchestration — drop-in for apis/imaging_classes.py:87-141 of the reference.
+
+``get_images`` no longer loops over passes in Python: every window of the list goes to the device in
+one batch, the class mean is produced by the fused correlate-and-stack kernel
+(``dvh_vsg_stack``), and ``self.images`` (the per-pass gathers) is materialised lazily, in one
+batched launch, only if a caller touches it.
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+
+from .. import engine
+from .dispersion_classes import SurfaceWaveDispersion
+from .virtual_shot_gather import VirtualShotGather, vsg_params
+
+
+class _LazyGathers(list):
+    """list of per-pass VirtualShotGather objects, computed on first access (one kernel launch)."""
+
+    def __init__(self, windows, prm):
+        super().__init__()
+        self._windows, self._prm, self._done = windows, prm, False
+
+    def _fill(self):
+        if not self._done:
+            self._done = True
+            res, geoms = engine.gathers(self._windows, self._prm)
+            super().extend(VirtualShotGather._from_arrays(w, x, g.gather_x_axis, g.gather_t_axis)
+                           for w, x, g in zip(self._windows, res, geoms))
+
+    def __len__(self):
+        self._fill()
+        return super().__len__()
+
+    def __iter__(self):
+        self._fill()
+        return super().__iter__()
+
+    def __getitem__(self, i):
+        self._fill()
+        return super().__getitem__(i)
+
+
+class ImagesFromWindows:
+    def __init__(self, windows, image_cls):
+        self.windows = windows
+        self.image_cls = image_cls
+
+    def get_images(self, norm=False, mute_offset=300, mute=True, **imaging_kwargs):
+        """Generic path (apis/imaging_classes.py:96-107): one image per window, then the mean."""
+        self.images = []
+        for window in self.windows:
+            if mute and not window.muted_along_traj:
+                window = copy.deepcopy(window)
+                window.mute_along_traj(offset=mute_offset)
+            self.images.append(self.image_cls(window, norm=norm, **imaging_kwargs))
+        self.avg_image = sum(self.images)
+        self.avg_image = self.avg_image / len(self.images)
+
+
+class DispersionImagesFromWindows(ImagesFromWindows):
+    def __init__(self, windows, image_cls=SurfaceWaveDispersion):
+        super().__init__(windows, image_cls)
+
+    def get_images(self, norm=False, mute_offset=300, mute=True, **imaging_kwargs):
+        """Batched flavour-B path: mute (HIP) + per-pass f-v maps stacked on device."""
+        from .dispersion_classes import batched_surface_wave_dispersion
+        windows = list(self.windows)
+        if mute:
+            windows = [copy.deepcopy(w) if not w.muted_along_traj else w for w in windows]
+            for w in windows:
+                if not w.muted_along_traj:
+                    w.mute_along_traj(offset=mute_offset)
+        self.images, self.avg_image = batched_surface_wave_dispersion(windows, norm=norm, **imaging_kwargs)
+
+
+class VirtualShotGathersFromWindows(ImagesFromWindows):
+    def __init__(self, windows, image_cls=VirtualShotGather):
+        super().__init__(windows, image_cls)
+
+    def get_images(self, norm=False, mute_offset=300, mute=False, **imaging_kwargs):
+        """apis/imaging_classes.py:137-138 forces norm=False, mute=False, then 96-107."""
+        windows = list(self.windows)
+        include_other_side = imaging_kwargs.pop("include_other_side", False)
+        prm = vsg_params(include_other_side, norm=False, **imaging_kwargs)
+        stack, geoms = engine.stacked(windows, prm)
+        self.images = _LazyGathers(windows, prm)
+        avg = stack[0].detach().to("cpu").numpy().astype(np.float64)
+        self.avg_image = VirtualShotGather._from_arrays(windows[0], avg, geoms[0].gather_x_axis,
+                                                        geoms[0].gather_t_axis)

@@ -1,0 +1,291 @@
+// Dispersion (f-v) image on MI355X (gfx950): map_fv of the reference, batched over gathers.
+//
+// Replaces fk (modules/utils.py:236-248) + map_fv (:457-475) + Dispersion (:383-426):
+//   FK = |fftshift(fft2(data, s=[nk, nf]))| sampled bilinearly at (k = f / v, f) with the queries
+//   clamped to the grid (interp2d(kind='linear') == FITPACK degree-1 spline), stored as float32,
+//   then savgol_filter(25, 4, axis=0, mode='interp') along frequency, output [Nvel, Nfreq].
+// Only the FK bins the queries touch are computed, as two GEMMs on the float64 MFMA pipe
+// (v_mfma_f64_16x16x4_f64): |FK| then tracks the reference's float64 fft2 to ~1e-13, so the
+// float32 f-v map (and its argmax pick) comes out as the reference's for exact inputs.
+//   1. time DFT   D[r, q]  = sum_t data[r, t] * exp(-2 pi i nu_q t / nf)      (r = gather x channel)
+//      real GEMM  [B*nch x nt] . [nt x 2*n_fb]  (cos | -sin float64 twiddles prepared on the host)
+//   2. channel contraction  Z[m, q] = sum_x exp(-2 pi i kappa_m x / nk) D[x, q]  per gather,
+//      complex GEMM as the real block GEMM [[Er, -Ei], [Ei, Er]] . [Dr; Di], then |Z| -> FK grid
+//      (optionally accumulated per class slot with a weight: the f-v image is linear in |FK|)
+//   3. f-v sampling: bilinear (FITPACK basis, double) -> float32 -> Savitzky-Golay operator (double)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "dvh_common.h"
+#include "dvh.h"
+
+namespace dvh {
+
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+
+// v_mfma_f64_16x16x4_f64 lane maps: A[i = l & 15][k = l >> 4], B[k = l >> 4][j = l & 15],
+// D[row = (l >> 4) + 4 r][col = l & 15] for r in [0, 4).
+__device__ __forceinline__ doublex4 mfma_f64(double a, double b, doublex4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+constexpr int kTM = 64, kTN = 64, kTK = 16, kPad = 16;
+
+// ---------------------------------------------------------------------------------------------
+// 1. time-DFT GEMM: C[r, n] = scale[r] * sum_k A[r, k] W[k, n]   (float64 MFMA, fp32 data)
+__global__ __launch_bounds__(256) void tdft_gemm_kernel(const float* __restrict__ data, int64_t b_stride,
+                                                         int64_t ch_stride, int32_t nch, int32_t M, int32_t K,
+                                                         const double* __restrict__ W, int32_t N,
+                                                         const float* __restrict__ row_scale,
+                                                         double* __restrict__ C) {
+  __shared__ double As[kTK][kTM + kPad];
+  __shared__ double Ws[kTK][kTN + kPad];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * kTM, n0 = blockIdx.x * kTN;
+  doublex4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < K; k0 += kTK) {
+    for (int e = threadIdx.x; e < kTM * kTK; e += 256) {
+      const int r = e / kTK, k = e % kTK;
+      const int gr = m0 + r, gk = k0 + k;
+      double v = 0.0;
+      if (gr < M && gk < K) {
+        const int b = gr / nch, x = gr % nch;
+        v = (double)data[(int64_t)b * b_stride + (int64_t)x * ch_stride + gk];
+      }
+      As[k][r] = v;
+    }
+    for (int e = threadIdx.x; e < kTK * kTN; e += 256) {
+      const int k = e / kTN, n = e % kTN;
+      const int gk = k0 + k, gn = n0 + n;
+      Ws[k][n] = (gk < K && gn < N) ? W[(int64_t)gk * N + gn] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kTK; kk += 4) {
+      double a[2], b[2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        a[f] = As[kk + (lane >> 4)][wm * 32 + f * 16 + (lane & 15)];
+        b[f] = Ws[kk + (lane >> 4)][wn * 32 + f * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_f64(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + i * 16 + (lane >> 4) + 4 * r;
+        const int col = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (row < M && col < N)
+          C[(int64_t)row * N + col] = acc[i][j][r] * (row_scale ? (double)row_scale[row] : 1.0);
+      }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 2. channel contraction + magnitude (float64 MFMA).  A (host table, global/L2) is [2*MT][K2],
+// K2 = 2*nch rounded up to a multiple of 4: rows [0, MT) give Re Z, rows [MT, 2MT) give Im Z.
+// One block = (gather b, 32 f-bins).
+constexpr int kFN = 32;
+
+__global__ __launch_bounds__(256) void fk_contract_kernel(const double* __restrict__ D, int32_t nch, int32_t n_fb,
+                                                           const double* __restrict__ Atab, int32_t MT, int32_t K2,
+                                                           int32_t n_kb, double* __restrict__ FK,
+                                                           const int32_t* __restrict__ slot,
+                                                           const float* __restrict__ weight) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int M2 = 2 * MT;
+  double* Bs = sm;                      // [K2][kFN + 1]
+  double* Cs = Bs + K2 * (kFN + 1);     // [M2][kFN + 1]
+  const int b = blockIdx.y, q0 = blockIdx.x * kFN;
+  const double* Db = D + (int64_t)b * nch * 2 * n_fb;
+  for (int e = threadIdx.x; e < K2 * kFN; e += 256) {
+    const int kk = e / kFN, n = e % kFN;
+    const int q = q0 + n;
+    double v = 0.0;
+    if (q < n_fb && kk < 2 * nch) {
+      const int x = kk < nch ? kk : kk - nch;
+      v = Db[(int64_t)x * 2 * n_fb + 2 * q + (kk < nch ? 0 : 1)];
+    }
+    Bs[kk * (kFN + 1) + n] = v;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n_mt = M2 / 16, n_nt = kFN / 16;
+  for (int t = wave; t < n_mt * n_nt; t += 4) {
+    const int mt = t / n_nt, nt = t % n_nt;
+    doublex4 acc = {0.0, 0.0, 0.0, 0.0};
+    const double* arow = Atab + (int64_t)(mt * 16 + (lane & 15)) * K2;
+    for (int kk = 0; kk < K2; kk += 4) {
+      const double a = arow[kk + (lane >> 4)];
+      const double bb = Bs[(kk + (lane >> 4)) * (kFN + 1) + nt * 16 + (lane & 15)];
+      acc = mfma_f64(a, bb, acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = mt * 16 + (lane >> 4) + 4 * r;
+      Cs[row * (kFN + 1) + nt * 16 + (lane & 15)] = acc[r];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < n_kb * kFN; e += 256) {
+    const int m = e / kFN, n = e % kFN, q = q0 + n;
+    if (q >= n_fb) continue;
+    const double mag = hypot(Cs[m * (kFN + 1) + n], Cs[(MT + m) * (kFN + 1) + n]);
+    if (slot) {
+      atomicAdd(FK + ((int64_t)slot[b] * n_kb + m) * n_fb + q, mag * (double)weight[b]);
+    } else {
+      FK[((int64_t)b * n_kb + m) * n_fb + q] = mag;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 3. f-v sampling + Savitzky-Golay.  One block = (gather b, 16 velocity rows), all frequencies.
+constexpr int kVC = 16;
+
+__global__ __launch_bounds__(256) void fv_kernel(const double* __restrict__ FK, int32_t n_kb, int32_t n_fb,
+                                                  const double* __restrict__ kgrid, double kmin, double kmax,
+                                                  const double* __restrict__ kq, int32_t nF, int32_t nV,
+                                                  const int32_t* __restrict__ fj, const double* __restrict__ fw,
+                                                  const double* __restrict__ sg, int32_t sgl,
+                                                  float* __restrict__ fv) {
+  extern __shared__ __attribute__((aligned(16))) float raw[];  // [nF][kVC]
+  const int b = blockIdx.y, v0 = blockIdx.x * kVC;
+  const double* F = FK + (int64_t)b * n_kb * n_fb;
+  const double k0 = kgrid[0], inv_dk = 1.0 / (kgrid[1] - kgrid[0]);
+  for (int e = threadIdx.x; e < nF * kVC; e += blockDim.x) {
+    const int f = e / kVC, iv = e % kVC, v = v0 + iv;
+    float val = 0.f;
+    if (v < nV) {
+      double q = kq[(int64_t)f * nV + v];
+      q = q < kmin ? kmin : (q > kmax ? kmax : q);  // fpbisp clamps to [t_b, t_e]
+      int m = (int)floor((q - k0) * inv_dk);
+      m = m < 0 ? 0 : (m > n_kb - 2 ? n_kb - 2 : m);
+      while (m < n_kb - 2 && q >= kgrid[m + 1]) ++m;
+      while (m > 0 && q < kgrid[m]) --m;
+      const double klo = kgrid[m], khi = kgrid[m + 1];
+      const double fx = 1.0 / (khi - klo);
+      const double hx0 = fx * (khi - q), hx1 = fx * (q - klo);  // fpbspl, degree 1
+      const int j = fj[f];
+      const double hy0 = fw[2 * f], hy1 = fw[2 * f + 1];
+      const double z00 = F[m * n_fb + j], z01 = F[m * n_fb + j + 1];
+      const double z10 = F[(m + 1) * n_fb + j], z11 = F[(m + 1) * n_fb + j + 1];
+      val = (float)(z00 * hx0 * hy0 + z01 * hx0 * hy1 + z10 * hx1 * hy0 + z11 * hx1 * hy1);
+    }
+    raw[f * kVC + iv] = val;
+  }
+  __syncthreads();
+  const int half = sgl / 2;
+  const double* h = sg;                        // interior taps, h[t] multiplies x[f - half + t]
+  const double* el = sg + sgl;                 // [half][sgl] left edge (fit to x[0:sgl])
+  const double* er = el + half * sgl;          // [half][sgl] right edge (fit to x[nF-sgl:nF])
+  for (int e = threadIdx.x; e < nF * kVC; e += blockDim.x) {
+    const int iv = e / nF, f = e % nF, v = v0 + iv;
+    if (v >= nV) continue;
+    double acc = 0.0;
+    if (f < half) {
+      for (int t = 0; t < sgl; ++t) acc += el[f * sgl + t] * (double)raw[t * kVC + iv];
+    } else if (f >= nF - half) {
+      const int r = f - (nF - half);
+      for (int t = 0; t < sgl; ++t) acc += er[r * sgl + t] * (double)raw[(nF - sgl + t) * kVC + iv];
+    } else {
+      for (int t = 0; t < sgl; ++t) acc += h[t] * (double)raw[(f - half + t) * kVC + iv];
+    }
+    fv[((int64_t)b * nV + v) * nF + f] = (float)acc;
+  }
+}
+
+// per-row L1 norms -> 1 / ||row||_1 (map_fv norm=True: data / norm(data, ord=1, axis=-1))
+__global__ __launch_bounds__(256) void row_l1_kernel(const float* __restrict__ data, int64_t b_stride,
+                                                      int64_t ch_stride, int32_t nch, int32_t nt,
+                                                      float* __restrict__ inv_l1) {
+  const int r = blockIdx.x;
+  const int b = r / nch, x = r % nch;
+  const float* row = data + (int64_t)b * b_stride + (int64_t)x * ch_stride;
+  double s = 0.0;
+  for (int t = threadIdx.x; t < nt; t += blockDim.x) s += fabs((double)row[t]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  __shared__ double part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) inv_l1[r] = (float)(1.0 / (part[0] + part[1] + part[2] + part[3]));
+}
+
+static int last_launch() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
+}
+
+}  // namespace dvh
+
+using namespace dvh;
+
+DVH_API int dvh_disp_row_l1(const float* data, int64_t b_stride, int64_t ch_stride, int32_t B, int32_t nch,
+                            int32_t nt, float* inv_l1, void* stream) {
+  if (!data || !inv_l1) return set_error(-2, "null pointer argument");
+  if (B * nch <= 0) return 0;
+  hipLaunchKernelGGL(row_l1_kernel, dim3(B * nch), dim3(256), 0, (hipStream_t)stream, data, b_stride, ch_stride, nch,
+                     nt, inv_l1);
+  return last_launch();
+}
+
+DVH_API int dvh_disp_tdft(const float* data, int64_t b_stride, int64_t ch_stride, int32_t B, int32_t nch,
+                          int32_t nt, const double* wt, int32_t n_fb, const float* row_scale, double* D,
+                          void* stream) {
+  if (!data || !wt || !D) return set_error(-2, "null pointer argument");
+  const int M = B * nch, N = 2 * n_fb;
+  if (M <= 0 || N <= 0) return 0;
+  dim3 grid((N + kTN - 1) / kTN, (M + kTM - 1) / kTM);
+  hipLaunchKernelGGL(tdft_gemm_kernel, grid, dim3(256), 0, (hipStream_t)stream, data, b_stride, ch_stride, nch, M, nt,
+                     wt, N, row_scale, D);
+  return last_launch();
+}
+
+DVH_API int dvh_disp_fk(const double* D, int32_t B, int32_t nch, int32_t n_fb, const double* atab, int32_t MT,
+                        int32_t K2, int32_t n_kb, double* FK, const int32_t* slot, const float* weight,
+                        void* stream) {
+  if (!D || !atab || !FK) return set_error(-2, "null pointer argument");
+  if ((slot == nullptr) != (weight == nullptr)) return set_error(-2, "slot and weight go together");
+  if (MT % 16 || n_kb > MT || K2 < 2 * nch || K2 % 4) return set_error(-2, "invalid contraction table shape");
+  if (B <= 0 || n_fb <= 0) return 0;
+  const size_t lds = sizeof(double) * ((size_t)K2 * (kFN + 1) + (size_t)2 * MT * (kFN + 1));
+  if (lds > 160 * 1024) return set_error(-4, "too many channels / wavenumbers for one block");
+  hipError_t e = hipFuncSetAttribute((const void*)fk_contract_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+  dim3 grid((n_fb + kFN - 1) / kFN, B);
+  hipLaunchKernelGGL(fk_contract_kernel, grid, dim3(256), lds, (hipStream_t)stream, D, nch, n_fb, atab, MT, K2, n_kb,
+                     FK, slot, weight);
+  return last_launch();
+}
+
+DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, const double* kgrid, double kmin,
+                        double kmax, const double* kq, int32_t nF, int32_t nV, const int32_t* fj, const double* fw,
+                        const double* sg, int32_t sgl, float* fv, void* stream) {
+  if (!FK || !kgrid || !kq || !fj || !fw || !sg || !fv) return set_error(-2, "null pointer argument");
+  if (n_kb < 2 || n_fb < 2) return set_error(-2, "FK grid needs at least 2 x 2 bins");
+  if (sgl % 2 == 0 || sgl > nF) return set_error(-4, "savgol window must be odd and <= number of frequencies");
+  if (B <= 0 || nV <= 0) return 0;
+  const size_t lds = sizeof(float) * (size_t)nF * kVC;
+  if (lds > 160 * 1024) return set_error(-4, "too many frequencies for one block");
+  hipError_t e = hipFuncSetAttribute((const void*)fv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+  dim3 grid((nV + kVC - 1) / kVC, B);
+  hipLaunchKernelGGL(fv_kernel, grid, dim3(256), lds, (hipStream_t)stream, FK, n_kb, n_fb, kgrid, kmin, kmax, kq, nF,
+                     nV, fj, fw, sg, sgl, fv);
+  return last_launch();
+}

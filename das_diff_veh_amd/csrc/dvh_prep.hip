@@ -1,0 +1,168 @@
+// Per-pass windowing, taper and bandpass on MI355X (gfx950).
+//
+//   dvh_sosfiltfilt  bandpass_data (modules/utils.py:179-189): scipy.signal.sosfiltfilt(sos, x, axis=1)
+//                    = odd extension by padlen, sosfilt with zi * x_ext[0], reverse, sosfilt with
+//                    zi * y[-1], reverse, trim.  One lane per trace, float64 recursion (the order-10
+//                    band edge at 1.2 Hz / 125 Hz puts poles within 1e-2 of the unit circle).
+//   dvh_mute_traj    SurfaceWaveWindow.mute_along_traj (apis/data_classes.py:49-72): column t is
+//                    multiplied by a tukey taper placed along the vehicle trajectory (host tables).
+//   dvh_mute_time    SurfaceWaveWindow.mute_along_time (apis/data_classes.py:100-104).
+// Data may be float32 (dtype 0) or float64 (dtype 1), modified in place.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dvh_common.h"
+#include "dvh.h"
+
+namespace dvh {
+
+constexpr int kMaxSec = 16;
+
+template <typename T>
+__global__ __launch_bounds__(64) void sosfiltfilt_kernel(T* __restrict__ x, int64_t n_rows, int64_t row_stride,
+                                                          int32_t n_t, const double* __restrict__ sos,
+                                                          int32_t n_sec, int32_t padlen,
+                                                          const double* __restrict__ zi,
+                                                          double* __restrict__ work) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  T* row = x + r * row_stride;
+  const int64_t n_ext = (int64_t)n_t + 2 * padlen;
+  double* y = work + r * n_ext;
+  double b0[kMaxSec], b1[kMaxSec], b2[kMaxSec], a1[kMaxSec], a2[kMaxSec], z0[kMaxSec], z1[kMaxSec];
+  for (int s = 0; s < n_sec; ++s) {
+    b0[s] = sos[6 * s];
+    b1[s] = sos[6 * s + 1];
+    b2[s] = sos[6 * s + 2];
+    a1[s] = sos[6 * s + 4];
+    a2[s] = sos[6 * s + 5];
+  }
+  const double x0 = (double)row[0], xn = (double)row[n_t - 1];
+  // ext[i]: i < padlen -> 2 x0 - x[padlen - i]; i >= padlen + n_t -> 2 xn - x[n_t - 2 - (i - padlen - n_t)]
+  auto ext = [&](int64_t i) -> double {
+    if (i < padlen) return 2.0 * x0 - (double)row[padlen - i];
+    const int64_t j = i - padlen;
+    if (j < n_t) return (double)row[j];
+    return 2.0 * xn - (double)row[n_t - 2 - (j - n_t)];
+  };
+  const double e0 = ext(0);
+  for (int s = 0; s < n_sec; ++s) {
+    z0[s] = zi[2 * s] * e0;
+    z1[s] = zi[2 * s + 1] * e0;
+  }
+  for (int64_t i = 0; i < n_ext; ++i) {
+    double v = ext(i);
+    for (int s = 0; s < n_sec; ++s) {
+      const double o = b0[s] * v + z0[s];
+      z0[s] = b1[s] * v - a1[s] * o + z1[s];
+      z1[s] = b2[s] * v - a2[s] * o;
+      v = o;
+    }
+    y[i] = v;
+  }
+  const double yl = y[n_ext - 1];
+  for (int s = 0; s < n_sec; ++s) {
+    z0[s] = zi[2 * s] * yl;
+    z1[s] = zi[2 * s + 1] * yl;
+  }
+  for (int64_t i = n_ext - 1; i >= 0; --i) {
+    double v = y[i];
+    for (int s = 0; s < n_sec; ++s) {
+      const double o = b0[s] * v + z0[s];
+      z0[s] = b1[s] * v - a1[s] * o + z1[s];
+      z1[s] = b2[s] * v - a2[s] * o;
+      v = o;
+    }
+    y[i] = v;
+  }
+  for (int32_t t = 0; t < n_t; ++t) row[t] = (T)y[padlen + t];
+}
+
+// tab[(p * n_t + t) * 3 + {0,1,2}] = {start, end, taper_start}; element (x, t) of pass p is scaled by
+// taper[taper_start + x - start] for start <= x < end and zeroed elsewhere.
+template <typename T>
+__global__ __launch_bounds__(256) void mute_traj_kernel(T* __restrict__ data, int64_t pass_stride, int32_t n_ch,
+                                                         int32_t n_t, const int32_t* __restrict__ tab,
+                                                         const double* __restrict__ taper) {
+  const int p = blockIdx.z;
+  const int x = blockIdx.y;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_t) return;
+  const int32_t* e = tab + ((int64_t)p * n_t + t) * 3;
+  T* v = data + (int64_t)p * pass_stride + (int64_t)x * n_t + t;
+  const int s = e[0], end = e[1];
+  if (x >= s && x < end) {
+    *v = (T)((double)*v * taper[e[2] + x - s]);
+  } else {
+    *v = (T)((double)*v * 0.0);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void mute_time_kernel(T* __restrict__ data, int64_t n_rows, int32_t n_t,
+                                                         const double* __restrict__ taper) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rows * n_t) return;
+  data[i] = (T)((double)data[i] * taper[i % n_t]);
+}
+
+static int last_launch() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
+}
+
+}  // namespace dvh
+
+using namespace dvh;
+
+DVH_API int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t,
+                            const double* sos, int32_t n_sec, int32_t padlen, const double* zi, double* work,
+                            void* stream) {
+  if (!x || !sos || !zi || !work) return set_error(-2, "null pointer argument");
+  if (n_sec <= 0 || n_sec > kMaxSec) return set_error(-4, "unsupported number of second-order sections");
+  if (n_t <= padlen) return set_error(-4, "The length of the input vector x must be greater than padlen");
+  if (padlen < 0 || n_t < 2) return set_error(-2, "invalid padlen / length");
+  if (n_rows <= 0) return 0;
+  const dim3 grid((unsigned)((n_rows + 63) / 64));
+  if (dtype == 0)
+    hipLaunchKernelGGL(sosfiltfilt_kernel<float>, grid, dim3(64), 0, (hipStream_t)stream, (float*)x, n_rows,
+                       row_stride, n_t, sos, n_sec, padlen, zi, work);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(sosfiltfilt_kernel<double>, grid, dim3(64), 0, (hipStream_t)stream, (double*)x, n_rows,
+                       row_stride, n_t, sos, n_sec, padlen, zi, work);
+  else
+    return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
+  return last_launch();
+}
+
+DVH_API int dvh_mute_traj(void* data, int32_t dtype, int32_t n_pass, int64_t pass_stride, int32_t n_ch, int32_t n_t,
+                          const int32_t* tab, const double* taper, void* stream) {
+  if (!data || !tab || !taper) return set_error(-2, "null pointer argument");
+  if (n_pass <= 0 || n_ch <= 0 || n_t <= 0) return 0;
+  const dim3 grid((n_t + 255) / 256, n_ch, n_pass);
+  if (dtype == 0)
+    hipLaunchKernelGGL(mute_traj_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (float*)data, pass_stride,
+                       n_ch, n_t, tab, taper);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(mute_traj_kernel<double>, grid, dim3(256), 0, (hipStream_t)stream, (double*)data, pass_stride,
+                       n_ch, n_t, tab, taper);
+  else
+    return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
+  return last_launch();
+}
+
+DVH_API int dvh_mute_time(void* data, int32_t dtype, int64_t n_rows, int32_t n_t, const double* taper, void* stream) {
+  if (!data || !taper) return set_error(-2, "null pointer argument");
+  if (n_rows <= 0 || n_t <= 0) return 0;
+  const int64_t n = n_rows * n_t;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (dtype == 0)
+    hipLaunchKernelGGL(mute_time_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (float*)data, n_rows, n_t,
+                       taper);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(mute_time_kernel<double>, grid, dim3(256), 0, (hipStream_t)stream, (double*)data, n_rows, n_t,
+                       taper);
+  else
+    return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
+  return last_launch();
+}

@@ -1,0 +1,117 @@
+"""Per-pass windowing / taper / bandpass on device (host side builds the small index tables).
+
+  bandpass_inplace  bandpass_data (modules/utils.py:179-189): butter(10, [flo, fhi] / fNy, 'band',
+                    output='sos') designed on the host (filter design, 10 x 6 coefficients), the
+                    zero-phase filtering itself in dvh_sosfiltfilt
+  mute_along_traj   apis/data_classes.py:49-72: per time sample the taper placement
+                    (argmax(x > car(t) - offset/2 + delta_x), clipped) is tabulated on the host with
+                    the reference's float64 expressions; the multiply runs in dvh_mute_traj
+  mute_along_time   apis/data_classes.py:100-104 -> dvh_mute_time
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.signal
+import torch
+
+from . import _lib
+from .device import default_device
+from .plan import interp1d_extrap
+
+
+def butter_bandpass_sos(dt, flo, fhi, order=10):
+    fny = 0.5 / dt
+    return scipy.signal.butter(order, [flo / fny, fhi / fny], analog=False, btype="band", output="sos")
+
+
+def _padlen(sos):
+    return 3 * (2 * len(sos) + 1 - min(int((sos[:, 2] == 0).sum()), int((sos[:, 5] == 0).sum())))
+
+
+def tukey(n, alpha):
+    """scipy.signal.windows.tukey(n, alpha) (sym=True)."""
+    return scipy.signal.windows.tukey(n, alpha)
+
+
+class _DeviceView:
+    """Device tensor for a host array or tensor, written back in place on exit."""
+
+    def __init__(self, data):
+        self.data = data
+        if isinstance(data, torch.Tensor) and data.is_cuda:
+            self.t = data if data.is_contiguous() else data.contiguous()
+        else:
+            host = np.asarray(data.detach().cpu() if isinstance(data, torch.Tensor) else data)
+            if host.dtype not in (np.float32, np.float64):
+                raise TypeError("data must be float32 or float64")
+            self.t = torch.from_numpy(np.ascontiguousarray(host)).to(default_device())
+        if self.t.dtype not in (torch.float32, torch.float64):
+            raise TypeError("data must be float32 or float64")
+        self.dtype = 0 if self.t.dtype == torch.float32 else 1
+
+    def write_back(self):
+        d = self.data
+        if isinstance(d, torch.Tensor):
+            if d.data_ptr() != self.t.data_ptr():
+                d.copy_(self.t)
+        else:
+            d[...] = self.t.to("cpu").numpy()
+
+
+def bandpass_inplace(data, dt, flo, fhi):
+    sos = butter_bandpass_sos(dt, flo, fhi)
+    zi = scipy.signal.sosfilt_zi(sos)
+    padlen = _padlen(sos)
+    v = _DeviceView(data)
+    t = v.t
+    n_t = t.shape[-1]
+    rows = t.reshape(-1, n_t)
+    if n_t <= padlen:
+        raise ValueError(f"The length of the input vector x must be greater than padlen, which is {padlen}.")
+    dev = t.device
+    sos_t = torch.from_numpy(np.ascontiguousarray(sos, dtype=np.float64)).to(dev)
+    zi_t = torch.from_numpy(np.ascontiguousarray(zi, dtype=np.float64)).to(dev)
+    work = torch.empty((rows.shape[0], n_t + 2 * padlen), dtype=torch.float64, device=dev)
+    _lib.call("dvh_sosfiltfilt", _lib.ptr(rows), v.dtype, rows.shape[0], rows.stride(0), n_t, _lib.ptr(sos_t),
+              len(sos), padlen, _lib.ptr(zi_t), _lib.ptr(work), _lib.stream_of(dev))
+    v.write_back()
+    return data
+
+
+def mute_traj_table(x_axis, t_axis, veh_state_x, veh_state_t, offset=200, alpha=0.3, delta_x=20):
+    """[T, 3] = (start, end, taper_start) per time sample and the taper, as the reference places them."""
+    f = interp1d_extrap(veh_state_t, veh_state_x)
+    car = f(np.asarray(t_axis, dtype=np.float64))
+    x_axis = np.asarray(x_axis, dtype=np.float64)
+    dx = x_axis[1] - x_axis[0]
+    nx = x_axis.size
+    n_samp = int(offset / dx)
+    center = car - offset / 2 + delta_x
+    c = np.argmax(x_axis[None, :] > center[:, None], axis=1)
+    s = np.maximum(0, c - n_samp // 2)
+    e = np.minimum(nx, c + n_samp // 2)
+    ts = s + n_samp // 2 - c
+    return np.stack([s, e, ts], axis=1).astype(np.int32), tukey(n_samp, alpha)
+
+
+def mute_along_traj(window, offset=200, alpha=0.3, delta_x=20):
+    tab, taper = mute_traj_table(window.x_axis, window.t_axis, window.veh_state_x, window.veh_state_t, offset, alpha,
+                                 delta_x)
+    v = _DeviceView(window.data)
+    n_ch, n_t = v.t.shape[-2], v.t.shape[-1]
+    dev = v.t.device
+    tab_t = torch.from_numpy(np.ascontiguousarray(tab)).to(dev)
+    taper_t = torch.from_numpy(np.ascontiguousarray(taper, dtype=np.float64)).to(dev)
+    _lib.call("dvh_mute_traj", _lib.ptr(v.t), v.dtype, 1, n_ch * n_t, n_ch, n_t, _lib.ptr(tab_t), _lib.ptr(taper_t),
+              _lib.stream_of(dev))
+    v.write_back()
+
+
+def mute_along_time(window, alpha=0.3):
+    v = _DeviceView(window.data)
+    n_t = v.t.shape[-1]
+    dev = v.t.device
+    taper_t = torch.from_numpy(np.ascontiguousarray(tukey(n_t, alpha), dtype=np.float64)).to(dev)
+    _lib.call("dvh_mute_time", _lib.ptr(v.t), v.dtype, v.t.numel() // n_t, n_t, _lib.ptr(taper_t),
+              _lib.stream_of(dev))
+    v.write_back()

@@ -1,0 +1,121 @@
+"""Batched, device-resident virtual-shot-gather entry points (the hot path).
+
+``windows`` is a CUDA (HIP) float32 tensor ``[n_pass, n_ch, n_t]`` (or any strided view whose time
+axis is contiguous); tables come from :class:`das_diff_veh_amd.plan.VsgPlan`.  All calls are
+stream-ordered on the current torch stream and never synchronise.
+
+    scales = vsg_scales(windows, plan)                 # per-pass amplitude normalisation, [n, 2]
+    g      = vsg_gathers(windows, plan, scales)        # per-pass gathers, [n, R, w]
+    s      = vsg_stack(windows, plan, slots, n_slot)   # mean gather per class slot, [n_slot, R, w]
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .plan import VsgPlan
+
+
+def _check_windows(windows: torch.Tensor, plan: VsgPlan):
+    if not windows.is_cuda:
+        raise ValueError("windows must be a device tensor (the hot path has no CPU fallback)")
+    if windows.dtype != torch.float32:
+        raise TypeError("windows must be float32")
+    if windows.dim() != 3 or windows.shape[0] != plan.n_pass:
+        raise ValueError(f"windows must be [n_pass={plan.n_pass}, C, T], got {tuple(windows.shape)}")
+    if windows.shape[1] < plan.n_ch or windows.shape[2] < plan.n_t or windows.stride(2) != 1:
+        raise ValueError("windows smaller than the plan or time axis not contiguous")
+
+
+def window_sumsq(windows: torch.Tensor) -> torch.Tensor:
+    out = torch.empty(windows.shape[0], dtype=torch.float64, device=windows.device)
+    _lib.call("dvh_window_sumsq", _lib.ptr(windows), windows.stride(0), windows.stride(1), windows.shape[0],
+              windows.shape[1], windows.shape[2], _lib.ptr(out), _lib.stream_of(windows.device))
+    return out
+
+
+def vsg_scales(windows: torch.Tensor, plan: VsgPlan, out: torch.Tensor | None = None) -> torch.Tensor:
+    _check_windows(windows, plan)
+    pass_tab, seg_tab = plan.device_tables(windows.device)
+    sumsq = None
+    if not plan.prm.norm and not plan.prm.norm_amp:
+        sumsq = window_sumsq(windows)
+    if out is None:
+        out = torch.empty((plan.n_pass, 2), dtype=torch.float32, device=windows.device)
+    _lib.call("dvh_vsg_scales", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
+              _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop, plan.flags, _lib.ptr(sumsq),
+              _lib.ptr(out), _lib.stream_of(windows.device))
+    return out
+
+
+def vsg_gathers(windows: torch.Tensor, plan: VsgPlan, scales: torch.Tensor | None = None,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    _check_windows(windows, plan)
+    if scales is None:
+        scales = vsg_scales(windows, plan)
+    pass_tab, seg_tab = plan.device_tables(windows.device)
+    if out is None:
+        out = torch.empty((plan.n_pass, plan.R, plan.w), dtype=torch.float32, device=windows.device)
+    _lib.call("dvh_vsg_gathers", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
+              _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop, plan.flags, _lib.ptr(scales),
+              _lib.ptr(out), _lib.stream_of(windows.device))
+    return out
+
+
+class StackSchedule:
+    """Passes sorted by class slot and cut into chunks that never straddle a slot.
+
+    ``weights[p] = 1 / count[slot(p)]`` so the kernel's accumulation is directly the class mean
+    (sum(images) / len(images)).  ``counts`` may be global counts (multi-GPU: each rank adds its
+    share of the mean and an all-reduce sums them).
+    """
+
+    def __init__(self, slots, n_slot, chunk=8, counts=None, device=None):
+        slots = np.asarray(slots, dtype=np.int64)
+        if slots.size and (slots.min() < 0 or slots.max() >= n_slot):
+            raise ValueError("slot id out of range")
+        self.n_slot = n_slot
+        order = np.argsort(slots, kind="stable")
+        local = np.bincount(slots, minlength=n_slot)
+        counts = local if counts is None else np.asarray(counts)
+        with np.errstate(divide="ignore"):
+            inv = np.where(counts > 0, 1.0 / np.maximum(counts, 1), 0.0)
+        self.weights = inv[slots].astype(np.float32)
+        chunks = []
+        pos = 0
+        for s in range(n_slot):
+            n = int(local[s])
+            for b in range(pos, pos + n, chunk):
+                chunks.append((b, min(b + chunk, pos + n), s))
+            pos += n
+        self.order = order.astype(np.int32)
+        self.chunk_tab = np.array(chunks, dtype=np.int32).reshape(-1, 3)
+        self.counts = counts
+        self._dev = {}
+
+    def device_tables(self, device):
+        key = str(device)
+        if key not in self._dev:
+            self._dev[key] = tuple(torch.from_numpy(np.ascontiguousarray(a)).to(device)
+                                   for a in (self.order, self.chunk_tab, self.weights))
+        return self._dev[key]
+
+
+def vsg_stack(windows: torch.Tensor, plan: VsgPlan, schedule: StackSchedule, scales: torch.Tensor | None = None,
+              out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
+    """Class-mean gathers [n_slot, R, w]; with accumulate=True adds into ``out``."""
+    _check_windows(windows, plan)
+    if scales is None:
+        scales = vsg_scales(windows, plan)
+    pass_tab, seg_tab = plan.device_tables(windows.device)
+    order, chunk_tab, weights = schedule.device_tables(windows.device)
+    if out is None:
+        out = torch.zeros((schedule.n_slot, plan.R, plan.w), dtype=torch.float32, device=windows.device)
+    elif not accumulate:
+        out.zero_()
+    _lib.call("dvh_vsg_stack", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
+              _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop, plan.flags, _lib.ptr(scales),
+              _lib.ptr(order), _lib.ptr(chunk_tab), int(chunk_tab.shape[0]), _lib.ptr(weights), _lib.ptr(out),
+              _lib.stream_of(windows.device))
+    return out

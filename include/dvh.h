@@ -1,0 +1,118 @@
+/*
+ * libdvh — MI355X (gfx950) C-ABI for the vehicle-pass imaging hot path of NohPei/das_diff_veh.
+ *
+ * The reference is pure Python; its "FFI" for this path is the Python call surface of
+ * apis/virtual_shot_gather.py, apis/dispersion_classes.py and modules/utils.py.  Each entry point
+ * below replaces the reference function cited next to it; the Python mirror of the reference API in
+ * das_diff_veh_amd/ binds them with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - every pointer is DEVICE memory owned by the caller (e.g. a torch tensor); nothing is
+ *     allocated inside;  `stream` is a hipStream_t (NULL = default stream); calls are
+ *     stream-ordered, asynchronous and graph-capturable (no host synchronisation inside)
+ *   - windows are float32, channel-major: sample (pass p, channel c, time t) is
+ *     win[p * pass_stride + c * ch_stride + t]  (strides in elements)
+ *   - return 0 on success; negative on error: -2 invalid argument, -3 HIP launch error,
+ *     -4 unsupported size; dvh_last_error() describes the calling thread's last error
+ */
+#ifndef DVH_H
+#define DVH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int dvh_abi_version(void);
+const char* dvh_last_error(void);
+
+/* ---------------------------------------------------------------- virtual shot gathers
+ * pass_tab [n_pass][2] = {row0 (= start_idx), pivot_idx};  gather row i is channel row0 + i.
+ * seg_tab  [n_pass][R][2 sides][2] = {slice start, slice length} of the row's time slice on the
+ *          forward (0) and other (1) side, exactly as the reference slices them
+ *          (apis/virtual_shot_gather.py:111-126, 14-43, 152, 172).
+ * w = int(wlen / dt), hop = int(w * 0.5) (modules/utils.py:255-256, 292-294).
+ * flags: 1 include_other_side, 2 norm (row L2), 4 norm_amp (divide by the pivot row's max).
+ */
+
+/* FFT length used for correlation windows of w samples (0 if unsupported). */
+int dvh_vsg_fft_length(int32_t w);
+
+/* ||window||_F^2 per pass (np.linalg.norm(window.data)**2, apis/virtual_shot_gather.py:125). */
+int dvh_window_sumsq(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, int32_t n_ch,
+                     int32_t n_t, double* out, void* stream);
+
+/* Per-pass, per-side amplitude normalisation: scales[p][side] = 1 / amax(pivot row)
+ * (post_processing_XCF, apis/virtual_shot_gather.py:137-138), or 1 / ||window||_F^2 when
+ * neither norm nor norm_amp is set (win_sumsq from dvh_window_sumsq). */
+int dvh_vsg_scales(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, const int32_t* pass_tab,
+                   const int32_t* seg_tab, int32_t R, int32_t w, int32_t hop, int32_t flags, const double* win_sumsq,
+                   float* scales, void* stream);
+
+/* Per-pass gathers out[n_pass][R][w]: VirtualShotGather(window, include_other_side, ...).XCF_out
+ * (apis/virtual_shot_gather.py:184-192 with construct_shot_gather[_other_side] :145-180,
+ * XCORR_vshot / XCORR_two_traces modules/utils.py:253-314). */
+int dvh_vsg_gathers(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, const int32_t* pass_tab,
+                    const int32_t* seg_tab, int32_t R, int32_t w, int32_t hop, int32_t flags, const float* scales,
+                    float* out, void* stream);
+
+/* Class stacks, accumulated: stack[slot][R][w] += sum_{p in slot} weight[p] * gather_p.
+ * With weight[p] = 1 / count[slot] this is sum(images) / len(images) per class
+ * (ImagesFromWindows.get_images, apis/imaging_classes.py:106-107; VirtualShotGather.__add__ /
+ * __truediv__ apis/virtual_shot_gather.py:195-210).  order[] lists passes grouped by slot;
+ * chunk_tab [n_chunk][3] = {begin, end (into order), slot}. */
+int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, const int32_t* pass_tab,
+                  const int32_t* seg_tab, int32_t R, int32_t w, int32_t hop, int32_t flags, const float* scales,
+                  const int32_t* order, const int32_t* chunk_tab, int32_t n_chunk, const float* weight, float* stack,
+                  void* stream);
+
+/* ---------------------------------------------------------------- dispersion (map_fv)
+ * Gathers data[B][nch][nt] (strides in elements).  Only the FK bins the (f, k = f / v) queries
+ * touch are formed: n_fb frequency bins (twiddles wt[nt][2 * n_fb] = cos | -sin) and n_kb
+ * wavenumber bins (atab [2 * MT][K2] float64 = [[Er, -Ei], [Ei, Er]], MT = 16 * ceil(n_kb / 16),
+ * K2 = 2 * nch rounded up to a multiple of 4).  Replaces fk (modules/utils.py:236-248) and map_fv (:457-475). */
+
+/* 1 / ||row||_1 per gather row (map_fv norm=True, modules/utils.py:461-464). */
+int dvh_disp_row_l1(const float* data, int64_t b_stride, int64_t ch_stride, int32_t B, int32_t nch, int32_t nt,
+                    float* inv_l1, void* stream);
+
+/* Time DFT on the float64 MFMA pipe: D[B * nch][2 * n_fb] float64 (re, im interleaved), rows
+ * scaled by row_scale (nullable).  wt[nt][2 * n_fb] float64. */
+int dvh_disp_tdft(const float* data, int64_t b_stride, int64_t ch_stride, int32_t B, int32_t nch, int32_t nt,
+                  const double* wt, int32_t n_fb, const float* row_scale, double* D, void* stream);
+
+/* Channel contraction (complex GEMM on MFMA) + |.|: FK[B][n_kb][n_fb]; with slot/weight
+ * (both non-NULL) FK[slot[b]] += weight[b] * |Z_b| instead (class mean of |FK|). */
+int dvh_disp_fk(const double* D, int32_t B, int32_t nch, int32_t n_fb, const double* atab, int32_t MT, int32_t K2,
+                int32_t n_kb, double* FK, const int32_t* slot, const float* weight, void* stream);
+
+/* f-v sampling: fv[B][nV][nF] = savgol(float32(bilinear(FK; k = kq[f][v], f)))  with the
+ * interp2d query order (kq sorted per frequency), FITPACK clamping to [kmin, kmax], the compact
+ * k grid kgrid[n_kb], per-frequency lower bin fj[nF] and weights fw[nF][2], and the
+ * Savitzky-Golay operator sg = {h[sgl], left[sgl/2][sgl], right[sgl/2][sgl]}. */
+int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, const double* kgrid, double kmin,
+                double kmax, const double* kq, int32_t nF, int32_t nV, const int32_t* fj, const double* fw,
+                const double* sg, int32_t sgl, float* fv, void* stream);
+
+/* ---------------------------------------------------------------- preprocessing
+ * dtype: 0 float32, 1 float64; data modified in place. */
+
+/* scipy.signal.sosfiltfilt(sos, x, axis=-1) per row (bandpass_data, modules/utils.py:179-189);
+ * zi = sosfilt_zi(sos) [n_sec][2]; work: n_rows * (n_t + 2 * padlen) doubles. */
+int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t, const double* sos,
+                    int32_t n_sec, int32_t padlen, const double* zi, double* work, void* stream);
+
+/* SurfaceWaveWindow.mute_along_traj (apis/data_classes.py:49-72): tab[n_pass][n_t][3] =
+ * {start, end, taper_start} per time sample; contiguous [n_ch][n_t] per pass. */
+int dvh_mute_traj(void* data, int32_t dtype, int32_t n_pass, int64_t pass_stride, int32_t n_ch, int32_t n_t,
+                  const int32_t* tab, const double* taper, void* stream);
+
+/* SurfaceWaveWindow.mute_along_time (apis/data_classes.py:100-104). */
+int dvh_mute_time(void* data, int32_t dtype, int64_t n_rows, int32_t n_t, const double* taper, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DVH_H */

@@ -1,0 +1,251 @@
+"""Generate the golden vectors under tests/golden/ by running the REFERENCE in this container.
+
+Run once, here (the survey container), never on the GPU box:
+
+    python tests/golden/make_golden.py
+
+It imports NohPei/das_diff_veh from /root/reference with the shims SURVEY.md §8(c) lists
+(stub modules for obspy/segyio/cv2, which the hot path never calls; numpy aliases for the
+``from scipy import arange, array, exp`` line removed from SciPy; an ``interp2d`` replacement,
+since SciPy >= 1.14 raises ``NotImplementedError`` for it and names ``RectBivariateSpline`` on a
+regular grid as the bug-for-bug replacement).  Nothing is written into /root/reference.
+
+Only data leaves this script: int16-quantised inputs (exact in fp32) and the reference's outputs.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+
+import numpy as np
+import scipy
+import scipy.interpolate
+import scipy.signal
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+from das_diff_veh_amd.synth import synth_pass, DT_W500, DT_W499  # noqa: E402
+
+REF = "/root/reference"
+
+
+class _Interp2dShim:
+    """interp2d(x, y, z, kind='linear') on a rectangular grid, as SciPy < 1.14 evaluated it.
+
+    regrid_smth with kx = ky = 1 and s = 0 reproduces the data at the knots; bisplev clamps
+    queries to the grid and __call__ sorts the query vectors (mergesort) before evaluating.
+    """
+
+    def __init__(self, x, y, z, kind="linear"):
+        assert kind == "linear"
+        x = np.ravel(x)
+        y = np.ravel(y)
+        z = np.asarray(z)
+        assert z.shape == (len(y), len(x))
+        self.spl = scipy.interpolate.RectBivariateSpline(x, y, z.T, kx=1, ky=1, s=0)
+
+    def __call__(self, x, y):
+        x = np.sort(np.atleast_1d(x), kind="mergesort")
+        y = np.sort(np.atleast_1d(y), kind="mergesort")
+        z = np.atleast_2d(self.spl(x, y)).T
+        if len(z) == 1:
+            z = z[0]
+        return np.array(z)
+
+
+def import_reference():
+    import matplotlib
+    matplotlib.use("Agg")
+    for name in ("obspy", "obspy.signal", "obspy.signal.filter", "segyio", "cv2"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["obspy.signal.filter"].bandpass = None
+    scipy.arange, scipy.array, scipy.exp = np.arange, np.array, np.exp
+    scipy.interpolate.interp2d = _Interp2dShim
+    sys.path.insert(0, REF)
+    import apis.data_classes as dc
+    import apis.virtual_shot_gather as vsg
+    import apis.dispersion_classes as dcl
+    import apis.imaging_classes as ic
+    import modules.utils as ut
+    return types.SimpleNamespace(dc=dc, vsg=vsg, dcl=dcl, ic=ic, ut=ut)
+
+
+def ref_window(ref, p, dtype=np.float64):
+    return ref.dc.SurfaceWaveWindow(
+        data=p["data"].astype(dtype), x_axis=p["x_axis"], t_axis=p["t_axis"], veh_state=p["veh_state"],
+        start_x_tracking=p["start_x_tracking"],
+        distance_along_fiber_tracking=p["distance_along_fiber_tracking"],
+        t_axis_tracking=p["t_axis_tracking"])
+
+
+def pack_inputs(passes, prefix=""):
+    out = {}
+    out[prefix + "q"] = np.stack([p["q"] for p in passes])
+    out[prefix + "x_axis"] = np.stack([p["x_axis"] for p in passes])
+    out[prefix + "t_axis"] = np.stack([p["t_axis"] for p in passes])
+    out[prefix + "veh_state"] = np.stack([p["veh_state"] for p in passes])
+    out[prefix + "start_x_tracking"] = np.array([p["start_x_tracking"] for p in passes])
+    out[prefix + "distance_along_fiber_tracking"] = passes[0]["distance_along_fiber_tracking"]
+    out[prefix + "t_axis_tracking"] = np.stack([p["t_axis_tracking"] for p in passes])
+    return out
+
+
+def gen_vsg(ref):
+    """Per-pass gathers, the class stack and its dispersion image (call stack A)."""
+    kw = dict(pivot=700, start_x=500, end_x=900, wlen=2)
+    passes = [synth_pass(100 + i) for i in range(5)]
+    wins = [ref_window(ref, p) for p in passes]
+    out = pack_inputs(passes)
+
+    # ImagesFromWindows.get_images path: norm=False, include_other_side=True (imaging_classes.py:137)
+    images = ref.ic.VirtualShotGathersFromWindows(wins)
+    images.get_images(include_other_side=True, **kw)
+    out["xcf"] = np.stack([im.XCF_out for im in images.images])
+    out["gather_x_axis"] = images.images[0].x_axis
+    out["gather_t_axis"] = images.images[0].t_axis
+    out["stack"] = images.avg_image.XCF_out
+    images.avg_image.compute_disp_image(end_x=0, start_x=-200)
+    out["fv_map"] = images.avg_image.disp.fv_map
+    out["fv_freqs"] = images.avg_image.disp.freqs
+    out["fv_vels"] = images.avg_image.disp.vels
+
+    # VirtualShotGather called directly: norm=True default; one-sided and two-sided
+    out["xcf_norm_2s"] = np.stack([ref.vsg.VirtualShotGather(w, include_other_side=True, **kw).XCF_out
+                                   for w in wins[:1]])
+    out["xcf_norm_1s"] = np.stack([ref.vsg.VirtualShotGather(w, include_other_side=False, **kw).XCF_out
+                                   for w in wins[:1]])
+    out["xcf_nonorm_1s"] = np.stack([ref.vsg.VirtualShotGather(w, include_other_side=False, norm=False, **kw).XCF_out
+                                     for w in wins[:1]])
+    # raw correlation scale: norm=False, norm_amp=False keeps the data / ||data||_F factor
+    out["xcf_raw_2s"] = np.stack([ref.vsg.VirtualShotGather(w, include_other_side=True, norm=False,
+                                                            norm_amp=False, **kw).XCF_out for w in wins[:1]])
+    # dispersion of the stack with the per-trace L1 normalisation (map_fv norm=True)
+    im = images.avg_image
+    s = np.abs(im.x_axis - (-200)).argmin()
+    e = np.abs(im.x_axis - 0).argmin()
+    d = ref.ut.Dispersion(im.XCF_out[s:e + 1], 8.16, im.t_axis[1] - im.t_axis[0],
+                          freqs=np.arange(0.8, 25, 0.1), vels=np.arange(200, 1200), norm=True)
+    out["fv_map_l1"] = d.fv_map
+    return out
+
+
+def gen_vsg_w499(ref):
+    """dt slightly above 0.004: w = 499 (prime), nsamp = 999, hop = 249."""
+    kw = dict(pivot=700, start_x=500, end_x=900, wlen=2)
+    passes = [synth_pass(200 + i, t0=DT_W499) for i in range(2)]
+    wins = [ref_window(ref, p) for p in passes]
+    out = pack_inputs(passes)
+    images = ref.ic.VirtualShotGathersFromWindows(wins)
+    images.get_images(include_other_side=True, **kw)
+    out["xcf"] = np.stack([im.XCF_out for im in images.images])
+    out["stack"] = images.avg_image.XCF_out
+    out["gather_t_axis"] = images.images[0].t_axis
+    images.avg_image.compute_disp_image(end_x=0, start_x=-200)
+    out["fv_map"] = images.avg_image.disp.fv_map
+    return out
+
+
+def gen_vsg_edge(ref):
+    """Edge cases: empty/wrapped slices, truncated windows, pivot near the aperture edge."""
+    out = {}
+    cases = [
+        # (name, synth kwargs, vsg kwargs)
+        ("early", dict(seed=300, tc_offset=-7.2), dict(pivot=700, start_x=500, end_x=900)),   # other side empty -> NaN side
+        ("late", dict(seed=301, tc_offset=5.5), dict(pivot=700, start_x=500, end_x=900)),     # fwd window truncated
+        ("slow", dict(seed=302, speed=12.0), dict(pivot=700, start_x=500, end_x=900)),        # far rows leave the window
+        ("p680", dict(seed=303, pivot=680.0), dict(pivot=680, start_x=480, end_x=880)),
+        ("narrow", dict(seed=304), dict(pivot=700, start_x=690, end_x=760)),
+        ("wlen1", dict(seed=305), dict(pivot=700, start_x=500, end_x=900, wlen=1, time_window_to_xcorr=3, delta_t=0.5)),
+    ]
+    for name, skw, vkw in cases:
+        seed = skw.pop("seed")
+        p = synth_pass(seed, **skw)
+        w = ref_window(ref, p)
+        for k, v in pack_inputs([p]).items():
+            out[f"{name}_{k}"] = v
+        g = ref.vsg.VirtualShotGather(w, include_other_side=True, norm=False, **vkw)
+        out[f"{name}_xcf"] = g.XCF_out
+        out[f"{name}_gx"] = g.x_axis
+        out[f"{name}_gt"] = g.t_axis
+        out[f"{name}_kw"] = np.array(repr(vkw))
+    # dt == 0.004 exactly: int(2 // dt) = 499 != int(2 / dt) = 500 -> the reference raises ValueError
+    p = synth_pass(306, t0=0.0)
+    try:
+        ref.vsg.VirtualShotGather(ref_window(ref, p), include_other_side=True, norm=False,
+                                  pivot=700, start_x=500, end_x=900)
+        out["dt004_raises"] = np.array(False)
+    except ValueError:
+        out["dt004_raises"] = np.array(True)
+    return out
+
+
+def gen_disp(ref):
+    """Per-pass dispersion flavour (SurfaceWaveDispersion, dispersion_classes.py:9-65) and mutes."""
+    out = {}
+    passes = [synth_pass(400 + i, n_t=2048) for i in range(3)]
+    for k, v in pack_inputs(passes).items():
+        out[k] = v
+    freqs = np.arange(0.8, 25, 0.1)
+    vels = np.arange(200, 1200, 2)
+    wins = [ref_window(ref, p) for p in passes]
+    naive = [ref.dcl.SurfaceWaveDispersion(w, freqs=freqs, vels=vels, method="naive", norm=False,
+                                           start_x=500, end_x=800) for w in wins]
+    out["naive_fv"] = np.stack([d.disp.fv_map for d in naive])
+    out["naive_stack"] = (sum(naive) / len(naive)).disp.fv_map
+    out["naive_l1_fv"] = ref.dcl.SurfaceWaveDispersion(wins[0], freqs=freqs, vels=vels, method="naive", norm=True,
+                                                       start_x=500, end_x=800).disp.fv_map
+    out["smart_fv"] = ref.dcl.SurfaceWaveDispersion(wins[1], freqs=freqs, vels=vels, method="smart",
+                                                    norm=False).disp.fv_map
+    # DispersionImagesFromWindows.get_images: mute_along_traj(offset=300) on a copy, naive disp, mean
+    imgs = ref.ic.DispersionImagesFromWindows(wins)
+    imgs.get_images(mute_offset=300, freqs=freqs, vels=vels, method="naive", start_x=500, end_x=800)
+    out["muted_stack"] = imgs.avg_image.disp.fv_map
+    out["freqs"] = freqs
+    out["vels"] = vels
+    # mute outputs themselves
+    import copy
+    w = copy.deepcopy(wins[2])
+    w.mute_along_traj(offset=300)
+    out["mute_traj_300"] = w.data.astype(np.float32)
+    w = copy.deepcopy(wins[2])
+    w.mute_along_time(alpha=0.3)
+    out["mute_time_03"] = w.data.astype(np.float32)
+    return out
+
+
+def gen_bandpass(ref):
+    """bandpass_data (modules/utils.py:179-189) as called at apis/timeLapseImaging.py:60."""
+    rng = np.random.default_rng(500)
+    n_ch, n_t = 8, 3000
+    t = np.arange(n_t) * 0.004
+    x = np.zeros((n_ch, n_t))
+    for f in (0.3, 0.9, 2.0, 7.5, 18.0, 33.0, 60.0):
+        x += np.cos(2 * np.pi * f * t[None, :] + rng.uniform(0, 6.28, (n_ch, 1)))
+    x += 0.3 * rng.standard_normal((n_ch, n_t))
+    q = np.round(x / 2 ** -12).astype(np.int16)
+    data = q.astype(np.float64) * 2 ** -12
+    y = data.copy()
+    ref.ut.bandpass_data(y, 0.004, 1.2, 30)
+    y2 = data.copy()
+    ref.ut.bandpass_data(y2, 0.004, 0.08, 1)
+    return dict(q=q, dt=np.array(0.004), out_1p2_30=y, out_0p08_1=y2)
+
+
+def main():
+    ref = import_reference()
+    meta = dict(numpy=np.__version__, scipy=scipy.__version__)
+    for name, fn in (("vsg_w500", gen_vsg), ("vsg_w499", gen_vsg_w499), ("vsg_edge", gen_vsg_edge),
+                     ("disp", gen_disp), ("bandpass", gen_bandpass)):
+        out = fn(ref)
+        out["meta"] = np.array(repr(meta))
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **out)
+        print(f"wrote {path}: {os.path.getsize(path) / 1e6:.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
