@@ -73,3 +73,48 @@ def synth_pass(seed, n_ch=56, n_t=4096, dx=8.16, x_first=472.0, t0=DT_W500, dt=0
 def linear_trajectory(x_axis_track, speed, tc, pivot):
     """(veh_state_x, veh_state_t) of a constant-speed pass, for batched synthetic workloads."""
     return x_axis_track, tc + (x_axis_track - pivot) / speed
+
+
+def synth_batch_device(n_pass, n_ch=60, n_t=5500, dx=8.16, x_first=None, t0=DT_W500, dt=0.004, pivot=700.0,
+                       seed=0, device="cuda", n_tones=8, noise=0.05, chunk=64, track_half=350):
+    """A batch of synthetic passes generated on the device (same wavefield model as synth_pass,
+    fewer tones), for throughput runs.  Returns (windows [n, C, T] float32, x_axis, t_axis,
+    per-pass tracked trajectories (veh_state_x, veh_state_t) on the 1 m / 50 Hz tracking grid,
+    speeds)."""
+    import torch
+    rng = np.random.default_rng(seed)
+    if x_first is None:
+        x_first = pivot - 30 * dx + 0.37
+    x_axis = x_first + dx * np.arange(n_ch)
+    t_axis = t0 + np.arange(n_t) * dt
+    speeds = rng.uniform(15.0, 30.0, n_pass)
+    tcs = t_axis[n_t // 2] + rng.uniform(-1.0, 1.0, n_pass)
+    freqs = rng.uniform(2.0, 25.0, n_tones)
+    phases = rng.uniform(0.0, 2.0 * np.pi, (n_pass, n_tones))
+    out = torch.empty((n_pass, n_ch, n_t), dtype=torch.float32, device=device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(int(seed) + 12345)
+    xs = torch.as_tensor(x_axis, dtype=torch.float32, device=device)[None, :, None]
+    for b in range(0, n_pass, chunk):
+        e = min(b + chunk, n_pass)
+        n = e - b
+        trel = torch.as_tensor(t_axis[None, :] - tcs[b:e, None], dtype=torch.float32, device=device)  # [n, T]
+        v = torch.as_tensor(speeds[b:e], dtype=torch.float32, device=device)[:, None]
+        xc = (pivot + v * trel)[:, None, :]                       # [n, 1, T]
+        d = (xs - xc).abs()                                      # [n, C, T]
+        amp = 1.0 / (1.0 + d / 50.0)
+        u = torch.zeros((n, n_ch, n_t), dtype=torch.float32, device=device)
+        ph = torch.as_tensor(phases[b:e], dtype=torch.float32, device=device)
+        for j, f in enumerate(freqs):
+            c = float(phase_velocity(f))
+            u += torch.cos(2.0 * np.pi * f * (trel[:, None, :] - d / c) + ph[:, j, None, None])
+        u *= amp * (2.0 / np.sqrt(n_tones))
+        u -= 1.5 * torch.exp(-(d / 15.0) ** 2)
+        u += noise * torch.randn((n, n_ch, n_t), generator=gen, dtype=torch.float32, device=device)
+        out[b:e] = torch.round(u / QUANT) * QUANT
+    xs_trk = np.arange(np.floor(pivot) - track_half, np.floor(pivot) + track_half + 1, 1.0)
+    trk = []
+    for v, tc in zip(speeds, tcs):
+        t = tc + (xs_trk - pivot) / v
+        trk.append((xs_trk, np.round(t / TRACK_DT) * TRACK_DT))
+    return out, x_axis, t_axis, trk, speeds

@@ -1,0 +1,76 @@
+"""World-size-2 gloo test of the multi-GPU data path on CPU (sharding + one all-reduce of the
+partial class stacks reproduces the single-process class means).  The partial stacks are formed
+with the oracle here (no GPU in this container); on the GPU box the same reduction runs over RCCL."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests import golden_io as gio
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from das_diff_veh_amd.distributed import allreduce_stacks, global_counts, shard_passes
+        from oracle import vsg
+        g = gio.load("vsg_w500")
+        n = gio.n_pass(g)
+        slots = np.array([0, 1, 0, 1, 1])[:n]
+        counts = global_counts(slots, 2)
+        mine = shard_passes(slots, world, rank)
+        part = torch.zeros((2,) + g["stack"].shape, dtype=torch.float64)
+        for i in mine:
+            x, _, _ = vsg.virtual_shot_gather(gio.oracle_window(g, int(i)), include_other_side=True, norm=False,
+                                              pivot=700, start_x=500, end_x=900, wlen=2)
+            part[slots[i]] += torch.from_numpy(x) / counts[slots[i]]
+        extra = torch.full((3,), float(rank + 1), dtype=torch.float64)
+        allreduce_stacks([part, extra])
+        q.put((rank, part.numpy(), extra.numpy(), mine.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_stack_reduction():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort()
+    from oracle import vsg
+    g = gio.load("vsg_w500")
+    slots = np.array([0, 1, 0, 1, 1])
+    ref = []
+    for s in range(2):
+        xs = [vsg.virtual_shot_gather(gio.oracle_window(g, i), include_other_side=True, norm=False, pivot=700,
+                                      start_x=500, end_x=900, wlen=2)[0] for i in np.flatnonzero(slots == s)]
+        ref.append(vsg.stack(xs))
+    for rank, stacks, extra, mine in out:
+        assert np.abs(stacks - np.stack(ref)).max() < 1e-12
+        assert np.array_equal(extra, np.full(3, 3.0))
+    assert sorted(out[0][3] + out[1][3]) == list(range(5))
+
+
+def test_shard_balance():
+    from das_diff_veh_amd.distributed import shard_passes
+    slots = np.repeat([0, 1, 2], [103, 1058, 734])
+    parts = [shard_passes(slots, 8, r) for r in range(8)]
+    assert sorted(np.concatenate(parts).tolist()) == list(range(slots.size))
+    for s in range(3):
+        per = [np.sum(slots[p] == s) for p in parts]
+        assert max(per) - min(per) <= 1

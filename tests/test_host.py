@@ -1,0 +1,179 @@
+"""Host-side logic (no GPU): index tables, the C-ABI library, schedules, dispersion tables."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import scipy.interpolate
+import scipy.signal
+
+from tests import golden_io as gio
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_interp1d_matches_scipy_bitwise():
+    from das_diff_veh_amd.plan import interp1d_extrap
+    rng = np.random.default_rng(0)
+    x = np.sort(rng.uniform(0, 1000, 200))
+    x = x[np.r_[True, np.diff(x) > 0]]
+    y = 3.0 + x / 17.3 + rng.normal(0, 0.01, x.size)
+    q = np.concatenate([rng.uniform(-100, 1100, 500), x[:10]])
+    ref = scipy.interpolate.interp1d(x[::-1], y[::-1], fill_value="extrapolate")(q)
+    assert np.array_equal(interp1d_extrap(x[::-1], y[::-1])(q), ref)
+
+
+def test_py_slice_semantics():
+    from das_diff_veh_amd.plan import py_slice
+    n = 17
+    for a in range(-25, 25):
+        for b in range(-25, 25):
+            s, L = py_slice(a, b, n)
+            ref = np.arange(n)[a:b]
+            assert L == ref.size and (L == 0 or s == ref[0])
+
+
+def test_first_true_ge():
+    from das_diff_veh_amd.plan import first_true_ge
+    t = 4.0 + np.arange(100) * 0.004
+    q = np.array([-1.0, 4.0, 4.0041, 4.396, 4.3961, 100.0, np.nan])
+    ref = np.array([np.argmax(t >= v) for v in q])
+    assert np.array_equal(first_true_ge(t, q), ref)
+
+
+@pytest.mark.parametrize("fixture", ["vsg_w500", "vsg_w499"])
+def test_plan_matches_oracle_slices(fixture):
+    """Every (start, length) the kernels will read is the slice the reference takes."""
+    from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+    from das_diff_veh_amd.plan import VsgParams, pass_geometry
+    g = gio.load(fixture)
+    prm = VsgParams(pivot=700, start_x=500, end_x=900, include_other_side=True, norm=False)
+    for i in range(gio.n_pass(g)):
+        w = SurfaceWaveWindow(**gio.pass_arrays(g, i))
+        geo = pass_geometry(w.x_axis, w.t_axis, w.veh_state_x, w.veh_state_t, prm)
+        f = scipy.interpolate.interp1d(w.veh_state_x, w.veh_state_t, fill_value="extrapolate")
+        T = w.t_axis.size
+        for side, sgn in ((0, 1), (1, -1)):
+            pt = int(np.argmax(w.t_axis >= f(700) + sgn * 1))
+            for r in range(geo.start_idx, geo.end_idx):
+                shared = r <= geo.pivot_idx if sgn > 0 else r >= geo.pivot_idx
+                if shared:
+                    sl = slice(pt, pt + geo.nsamp) if sgn > 0 else slice(pt - geo.nsamp, pt)
+                else:
+                    ti = int(np.argmax(w.t_axis >= f(w.x_axis[r]) + sgn * 1))
+                    sl = slice(ti, ti + geo.nsamp) if sgn > 0 else slice(ti - geo.nsamp, ti)
+                idx = np.arange(T)[sl]
+                a, L = geo.seg[r - geo.start_idx, side]
+                assert L == idx.size and (L == 0 or a == idx[0]), (i, side, r)
+
+
+def test_plan_rejects_dt_004():
+    from das_diff_veh_amd.plan import VsgParams, pass_geometry
+    t = np.arange(1000) * 0.004
+    with pytest.raises(ValueError):
+        pass_geometry(np.arange(60) * 8.16 + 460, t, np.arange(300.0, 1000.0), np.linspace(0, 4, 700),
+                      VsgParams(pivot=700, start_x=500, end_x=900))
+
+
+def test_stack_schedule():
+    from das_diff_veh_amd.vsg import StackSchedule
+    slots = np.array([2, 0, 1, 1, 0, 2, 2, 2, 1, 0, 0])
+    s = StackSchedule(slots, 3, chunk=2)
+    seen = np.zeros(slots.size, int)
+    for b, e, slot in s.chunk_tab:
+        assert e - b <= 2
+        for q in range(b, e):
+            assert slots[s.order[q]] == slot
+            seen[s.order[q]] += 1
+    assert (seen == 1).all()
+    np.testing.assert_allclose(s.weights, 1.0 / np.bincount(slots)[slots])
+
+
+def test_savgol_operator_matches_scipy():
+    from das_diff_veh_amd.disp import savgol_operator
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal(242).astype(np.float32)
+    h, el, er = savgol_operator(25, 4)
+    y = np.empty(242)
+    for f in range(242):
+        if f < 12:
+            y[f] = el[f] @ x[:25]
+        elif f >= 230:
+            y[f] = er[f - 230] @ x[-25:]
+        else:
+            y[f] = h @ x[f - 12:f + 13]
+    ref = scipy.signal.savgol_filter(x, 25, 4)
+    assert np.abs(y - ref).max() < 1e-5
+
+
+def test_disp_plan_reproduces_reference_bilinear_on_host():
+    """The host tables + kernel formula (evaluated here in numpy) give the oracle's f-v map."""
+    from das_diff_veh_amd.disp import DispPlan
+    from oracle import disp as odisp
+    g = gio.load("vsg_w500")
+    s = np.abs(g["gather_x_axis"] + 200).argmin()
+    e = np.abs(g["gather_x_axis"] - 0).argmin()
+    data = g["stack"][s:e + 1]
+    dt = g["gather_t_axis"][1] - g["gather_t_axis"][0]
+    freqs, vels = np.arange(0.8, 25, 0.1), np.arange(200, 1200)
+    p = DispPlan(data.shape[0], data.shape[1], 8.16, dt, freqs, vels)
+    res, _, _ = odisp.fk(data, 8.16, dt)
+    fk = res[p.m_lo:p.m_lo + p.n_kb, p.j_lo:p.j_lo + p.n_fb]
+    # the twiddle tables reproduce the full fft2 on the compact grid
+    D = data @ (p.wt[:, 0::2] + 1j * p.wt[:, 1::2])
+    Z = (p.atab[:p.n_kb, :data.shape[0]] + 1j * p.atab[p.MT:p.MT + p.n_kb, :data.shape[0]]) @ D
+    np.testing.assert_allclose(np.abs(Z), fk, rtol=1e-9, atol=1e-9 * fk.max())
+    raw = np.empty((p.nF, p.nV))
+    for f in range(p.nF):
+        q = np.clip(p.kq[f], p.kmin, p.kmax)
+        m = np.clip(np.searchsorted(p.kgrid, q, side="right") - 1, 0, p.n_kb - 2)
+        klo, khi = p.kgrid[m], p.kgrid[m + 1]
+        fx = 1.0 / (khi - klo)
+        hx0, hx1 = fx * (khi - q), fx * (q - klo)
+        j = p.fj[f]
+        hy0, hy1 = p.fw[f]
+        raw[f] = fk[m, j] * hx0 * hy0 + fk[m, j + 1] * hx0 * hy1 + fk[m + 1, j] * hx1 * hy0 + \
+            fk[m + 1, j + 1] * hx1 * hy1
+    fv = scipy.signal.savgol_filter(raw.astype(np.float32), 25, 4, axis=0).T
+    assert np.abs(fv - g["fv_map"]).max() <= 1e-6 * np.abs(g["fv_map"]).max()
+
+
+def test_library_exports_every_header_symbol():
+    """libdvh.so loads without a GPU and exports every entry point include/dvh.h declares."""
+    from das_diff_veh_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        from das_diff_veh_amd.build import build
+        build()
+    hdr = open(os.path.join(ROOT, "include", "dvh.h")).read()
+    declared = set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(dvh_\w+)\(", hdr, flags=re.M))
+    assert len(declared) >= 14
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
+    assert _lib.load().dvh_abi_version() == 1
+    assert _lib.load().dvh_vsg_fft_length(500) == 500
+    assert _lib.load().dvh_vsg_fft_length(499) == 1024
+    assert _lib.load().dvh_vsg_fft_length(5000) == 0
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("has a GPU")
+    from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+    from das_diff_veh_amd.apis.virtual_shot_gather import VirtualShotGather
+    g = gio.load("vsg_w500")
+    w = SurfaceWaveWindow(**gio.pass_arrays(g, 0))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        VirtualShotGather(w, include_other_side=True, pivot=700, start_x=500, end_x=900)
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "das_diff_veh_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith(".py"):
+                src = open(os.path.join(dp, f)).read()
+                assert "import oracle" not in src and "from oracle" not in src, f

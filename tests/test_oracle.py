@@ -1,0 +1,114 @@
+"""The oracle (CPU restatement) against the reference's golden vectors: this is what pins it."""
+import ast
+
+import numpy as np
+import pytest
+
+from tests import golden_io as gio
+
+KW = dict(pivot=700, start_x=500, end_x=900, wlen=2)
+
+
+@pytest.mark.parametrize("fixture", ["vsg_w500", "vsg_w499"])
+def test_vsg_per_pass_and_stack(fixture):
+    from oracle import vsg
+    g = gio.load(fixture)
+    xs = []
+    for i in range(gio.n_pass(g)):
+        x, gx, gt = vsg.virtual_shot_gather(gio.oracle_window(g, i), include_other_side=True, norm=False, **KW)
+        assert np.abs(x - g["xcf"][i]).max() < 1e-12
+        xs.append(x)
+    assert np.abs(vsg.stack(xs) - g["stack"]).max() < 1e-12
+    assert np.array_equal(gt, g["gather_t_axis"])
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("xcf_norm_2s", dict(include_other_side=True)),
+    ("xcf_norm_1s", dict(include_other_side=False)),
+    ("xcf_nonorm_1s", dict(include_other_side=False, norm=False)),
+    ("xcf_raw_2s", dict(include_other_side=True, norm=False, norm_amp=False)),
+])
+def test_vsg_variants(name, kw):
+    from oracle import vsg
+    g = gio.load("vsg_w500")
+    x, _, _ = vsg.virtual_shot_gather(gio.oracle_window(g, 0), **kw, **KW)
+    ref = g[name][0]
+    assert np.array_equal(np.isnan(x), np.isnan(ref))
+    m = np.isfinite(ref)
+    assert np.abs(x[m] - ref[m]).max() <= 1e-12 * max(1.0, np.abs(ref[m]).max())
+
+
+@pytest.mark.parametrize("case", ["early", "late", "slow", "p680", "narrow", "wlen1"])
+def test_vsg_edges(case):
+    from oracle import vsg
+    g = gio.load("vsg_edge")
+    kw = ast.literal_eval(str(g[case + "_kw"]))
+    x, gx, gt = vsg.virtual_shot_gather(gio.oracle_window(g, 0, case + "_"), include_other_side=True, norm=False,
+                                        **kw)
+    ref = g[case + "_xcf"]
+    assert x.shape == ref.shape
+    assert np.array_equal(np.isnan(x), np.isnan(ref)) and np.array_equal(np.isinf(x), np.isinf(ref))
+    m = np.isfinite(ref)
+    if m.any():
+        assert np.abs(x[m] - ref[m]).max() < 1e-12
+    assert np.array_equal(gx, g[case + "_gx"]) and np.array_equal(gt, g[case + "_gt"])
+
+
+def test_vsg_dt_exact_raises_like_reference():
+    from das_diff_veh_amd.synth import synth_pass
+    from oracle import vsg
+    g = gio.load("vsg_edge")
+    assert bool(g["dt004_raises"])
+    p = synth_pass(306, t0=0.0)
+    w = vsg.window_from_arrays(p["q"], p["x_axis"], p["t_axis"], p["veh_state"], p["start_x_tracking"],
+                               p["distance_along_fiber_tracking"], p["t_axis_tracking"])
+    with pytest.raises(ValueError):
+        vsg.virtual_shot_gather(w, include_other_side=True, norm=False, **KW)
+
+
+def test_disp_stack_images():
+    from oracle import disp
+    g = gio.load("vsg_w500")
+    fv = disp.compute_disp_image(g["stack"], g["gather_x_axis"], g["gather_t_axis"], start_x=-200, end_x=0)
+    assert np.array_equal(fv, g["fv_map"])
+    fv = disp.compute_disp_image(g["stack"], g["gather_x_axis"], g["gather_t_axis"], start_x=-200, end_x=0, norm=True)
+    assert np.array_equal(fv, g["fv_map_l1"])
+
+
+def test_disp_per_pass_and_mutes():
+    from oracle import disp, preprocess, vsg
+    g = gio.load("disp")
+    fr, vl = g["freqs"], g["vels"]
+    wins = [gio.oracle_window(g, i) for i in range(gio.n_pass(g))]
+    fvs = [disp.naive_disp(w["data"], w["x_axis"], w["t_axis"], fr, vl, 500, 800, norm=False) for w in wins]
+    for i, fv in enumerate(fvs):
+        assert np.array_equal(fv, g["naive_fv"][i])
+    assert np.abs(sum(fvs) / 3 - g["naive_stack"]).max() == 0
+    w = wins[2]
+    m = preprocess.mute_along_traj(w["data"], w["x_axis"], w["t_axis"], w["veh_state_x"], w["veh_state_t"], 300)
+    assert np.array_equal(m.astype(np.float32), g["mute_traj_300"])
+    assert np.array_equal(preprocess.mute_along_time(w["data"], 0.3).astype(np.float32), g["mute_time_03"])
+    _ = vsg
+
+
+def test_bandpass():
+    from oracle import preprocess
+    g = gio.load("bandpass")
+    x = g["q"][:2].astype(np.float64) * 2.0 ** -12
+    y = preprocess.bandpass_data(x, float(g["dt"]), 1.2, 30)
+    assert np.abs(y - g["out_1p2_30"][:2]).max() < 1e-12
+
+
+def test_ref_loop_baseline_matches_reference():
+    """The CPU baseline bench.py times computes the reference's results."""
+    from oracle import ref_loop
+    g = gio.load("vsg_w500")
+    gs = []
+    for i in range(2):
+        w = gio.oracle_window(g, i)
+        x, gx, gt = ref_loop.gather(w["data"], w["x_axis"], w["t_axis"], w["veh_state_x"], w["veh_state_t"], 700, 500,
+                                    900)
+        assert np.abs(x - g["xcf"][i]).max() < 1e-12
+        gs.append(x)
+    fv = ref_loop.disp_image(g["stack"], g["gather_x_axis"], g["gather_t_axis"])
+    assert np.abs(fv - g["fv_map"]).max() <= 1e-6 * np.abs(g["fv_map"]).max()
