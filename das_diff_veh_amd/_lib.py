@@ -12,7 +12,7 @@ import os
 import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "libdvh.so")
+LIB_PATH = os.environ.get("DVH_LIB") or os.path.join(_PKG, "lib", "libdvh.so")
 
 _i32, _i64, _p, _f32, _f64 = C.c_int32, C.c_int64, C.c_void_p, C.c_float, C.c_double
 

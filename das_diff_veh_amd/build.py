@@ -45,7 +45,17 @@ def _compile(src, verbose=False):
     return obj
 
 
-def build(verbose=False, jobs=None):
+def build(verbose=False, jobs=None, out=None, defines=()):
+    """Build libdvh.so (or, with out/defines, a variant library for A/B timing)."""
+    global LIB, OBJ_DIR, CFLAGS
+    if out is not None:
+        saved = LIB, OBJ_DIR, CFLAGS
+        LIB, OBJ_DIR = out, out + ".obj"
+        CFLAGS = CFLAGS + [f"-D{d}" for d in defines]
+        try:
+            return build(verbose, jobs)
+        finally:
+            LIB, OBJ_DIR, CFLAGS = saved
     os.makedirs(OBJ_DIR, exist_ok=True)
     srcs = _sources()
     jobs = jobs or min(len(srcs), 8)
@@ -63,4 +73,8 @@ def build(verbose=False, jobs=None):
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    args = [a for a in sys.argv[1:] if a != "-v"]
+    if args:  # python -m das_diff_veh_amd.build OUT.so DEFINE=1 ...
+        print(build(verbose="-v" in sys.argv, out=os.path.abspath(args[0]), defines=args[1:]))
+    else:
+        print(build(verbose="-v" in sys.argv))

@@ -30,56 +30,49 @@ __device__ __forceinline__ doublex4 mfma_f64(double a, double b, doublex4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-constexpr int kTM = 64, kTN = 64, kTK = 16, kPad = 16;
-
 // ---------------------------------------------------------------------------------------------
 // 1. time-DFT GEMM: C[r, n] = scale[r] * sum_k A[r, k] W[k, n]   (float64 MFMA, fp32 data)
-__global__ __launch_bounds__(256) void tdft_gemm_kernel(const float* __restrict__ data, int64_t b_stride,
-                                                         int64_t ch_stride, int32_t nch, int32_t M, int32_t K,
-                                                         const double* __restrict__ W, int32_t N,
-                                                         const float* __restrict__ row_scale,
-                                                         double* __restrict__ C) {
-  __shared__ double As[kTK][kTM + kPad];
-  __shared__ double Ws[kTK][kTN + kPad];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * kTM, n0 = blockIdx.x * kTN;
+// One wave per 32 x 32 output tile and K slice (split-K): the problem is small (tens of gather rows
+// x a few hundred bins), so K is split to put hundreds of waves on the chip; the slices are summed
+// with float64 atomics into C (zeroed by the launcher).
+constexpr int kGT = 32;
+
+__global__ __launch_bounds__(64) void tdft_gemm_kernel(const float* __restrict__ data, int64_t b_stride,
+                                                        int64_t ch_stride, int32_t nch, int32_t M, int32_t K,
+                                                        const double* __restrict__ W, int32_t N,
+                                                        const float* __restrict__ row_scale, int32_t kslice,
+                                                        double* __restrict__ C) {
+  const int lane = threadIdx.x;
+  const int m0 = blockIdx.y * kGT, n0 = blockIdx.x * kGT;
+  const int k0 = blockIdx.z * kslice, k1 = min(K, k0 + kslice);
+  const float* rowp[2];
+  bool rok[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const int r = m0 + f * 16 + (lane & 15);
+    rok[f] = r < M;
+    const int rr = rok[f] ? r : 0;
+    rowp[f] = data + (int64_t)(rr / nch) * b_stride + (int64_t)(rr % nch) * ch_stride;
+  }
   doublex4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = doublex4{0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < K; k0 += kTK) {
-    for (int e = threadIdx.x; e < kTM * kTK; e += 256) {
-      const int r = e / kTK, k = e % kTK;
-      const int gr = m0 + r, gk = k0 + k;
-      double v = 0.0;
-      if (gr < M && gk < K) {
-        const int b = gr / nch, x = gr % nch;
-        v = (double)data[(int64_t)b * b_stride + (int64_t)x * ch_stride + gk];
-      }
-      As[k][r] = v;
+  for (int k = k0; k < k1; k += 4) {
+    const int kk = k + (lane >> 4);
+    const bool kok = kk < k1;
+    double a[2], b[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      a[f] = (kok && rok[f]) ? (double)rowp[f][kk] : 0.0;
+      const int c = n0 + f * 16 + (lane & 15);
+      b[f] = (kok && c < N) ? W[(int64_t)kk * N + c] : 0.0;
     }
-    for (int e = threadIdx.x; e < kTK * kTN; e += 256) {
-      const int k = e / kTN, n = e % kTN;
-      const int gk = k0 + k, gn = n0 + n;
-      Ws[k][n] = (gk < K && gn < N) ? W[(int64_t)gk * N + gn] : 0.0;
-    }
-    __syncthreads();
 #pragma unroll
-    for (int kk = 0; kk < kTK; kk += 4) {
-      double a[2], b[2];
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        a[f] = As[kk + (lane >> 4)][wm * 32 + f * 16 + (lane & 15)];
-        b[f] = Ws[kk + (lane >> 4)][wn * 32 + f * 16 + (lane & 15)];
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_f64(a[i], b[j], acc[i][j]);
-    }
-    __syncthreads();
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_f64(a[i], b[j], acc[i][j]);
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -87,10 +80,10 @@ __global__ __launch_bounds__(256) void tdft_gemm_kernel(const float* __restrict_
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 32 + i * 16 + (lane >> 4) + 4 * r;
-        const int col = n0 + wn * 32 + j * 16 + (lane & 15);
+        const int row = m0 + i * 16 + (lane >> 4) + 4 * r;
+        const int col = n0 + j * 16 + (lane & 15);
         if (row < M && col < N)
-          C[(int64_t)row * N + col] = acc[i][j][r] * (row_scale ? (double)row_scale[row] : 1.0);
+          atomicAdd(C + (int64_t)row * N + col, acc[i][j][r] * (row_scale ? (double)row_scale[row] : 1.0));
       }
 }
 
@@ -249,9 +242,17 @@ DVH_API int dvh_disp_tdft(const float* data, int64_t b_stride, int64_t ch_stride
   if (!data || !wt || !D) return set_error(-2, "null pointer argument");
   const int M = B * nch, N = 2 * n_fb;
   if (M <= 0 || N <= 0) return 0;
-  dim3 grid((N + kTN - 1) / kTN, (M + kTM - 1) / kTM);
-  hipLaunchKernelGGL(tdft_gemm_kernel, grid, dim3(256), 0, (hipStream_t)stream, data, b_stride, ch_stride, nch, M, nt,
-                     wt, N, row_scale, D);
+  hipError_t e = hipMemsetAsync(D, 0, sizeof(double) * (size_t)M * N, (hipStream_t)stream);
+  if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+  const int tiles = ((M + kGT - 1) / kGT) * ((N + kGT - 1) / kGT);
+  // enough K slices for ~1024 waves, at least 64 samples each
+  int splits = (1024 + tiles - 1) / tiles;
+  int kslice = (nt + splits - 1) / splits;
+  kslice = kslice < 64 ? 64 : ((kslice + 3) / 4) * 4;
+  splits = (nt + kslice - 1) / kslice;
+  dim3 grid((N + kGT - 1) / kGT, (M + kGT - 1) / kGT, splits);
+  hipLaunchKernelGGL(tdft_gemm_kernel, grid, dim3(64), 0, (hipStream_t)stream, data, b_stride, ch_stride, nch, M, nt,
+                     wt, N, row_scale, kslice, D);
   return last_launch();
 }
 

@@ -63,64 +63,87 @@ __device__ __forceinline__ int pmod(int a, int m) {
   return r < 0 ? r + m : r;
 }
 
-// Accumulate sum_s P_s[f] * conj(R_s[f]) for one side into C (lane owns bins f = lane + 64 j).
+__device__ __forceinline__ int n_subwin(int L, int w, int hop) { return (L >= w) ? (L - w) / hop + 1 : 0; }
+
+// Wave-uniform value (keeps table indices and table entries in SGPRs -> scalar loads).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Global -> register staging of one sub-window z = pivot + i * receiver (lane owns n = lane + 64 j).
 template <int N>
-__device__ __forceinline__ int side_spectrum(const float* __restrict__ piv, const float* __restrict__ rcv,
-                                             int a, int L, int w, int hop, float2* bufA, float2* bufB,
-                                             const float2* tw, int lane, float2 (&C)[(N + 63) / 64]) {
+__device__ __forceinline__ void load_subwin(const float* __restrict__ piv, const float* __restrict__ rcv, int a,
+                                            int w, int lane, float2 (&z)[(N + 63) / 64]) {
   constexpr int NJ = (N + 63) / 64;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) C[j] = make_float2(0.f, 0.f);
-  const int nwin = (L >= w) ? (L - w) / hop + 1 : 0;
-  for (int s = 0; s < nwin; ++s) {
-    const float* pp = piv + a + s * hop;
-    const float* rr = rcv + a + s * hop;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = lane + 64 * j;
-      if (n < N) bufA[n] = (n < w) ? make_float2(pp[n], rr[n]) : make_float2(0.f, 0.f);
-    }
-    wave_sync();
-    const float2* X = FftPlan<N>::T::run(bufA, bufB, tw, lane);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int f = lane + 64 * j;
-      if (f < N) {
-        const float2 A = X[f];
-        const float2 Bc = X[f == 0 ? 0 : N - f];  // B = conj(Bc)
-        const float bx = Bc.x, by = -Bc.y;
-        // P = (A + B) / 2, R = (A - B) / 2i  ->  P conj(R) = (i / 4) (A + B) conj(A - B)
-        C[j].x += 0.5f * (bx * A.y - by * A.x);
-        C[j].y += 0.25f * ((A.x * A.x + A.y * A.y) - (bx * bx + by * by));
-      }
-    }
-    wave_sync();
+  for (int j = 0; j < NJ; ++j) {
+    const int n = lane + 64 * j;
+    z[j] = (n < w) ? make_float2(piv[a + n], rcv[a + n]) : make_float2(0.f, 0.f);
   }
-  return nwin;
 }
 
 // Both sides of one gather row -> raw correlations in LDS: Y[k].x = N * sum_s c_f, -Y[k].y = N * sum_s c_o.
+// The sub-windows of both sides form one sequence q = 0 .. nwf + nwo - 1; the global loads of
+// sub-window q + 1 are issued before the FFT of sub-window q so their latency hides under it.
 template <int N>
 __device__ __forceinline__ const float2* row_correlations(const VsgArgs& A, int p, int i, bool other,
                                                           float2* bufA, float2* bufB, const float2* tw,
                                                           int lane, int& nwin_f, int& nwin_o, int& ch,
                                                           int& pivot) {
   constexpr int NJ = (N + 63) / 64;
-  const int row0 = A.pass_tab[2 * p];
-  pivot = A.pass_tab[2 * p + 1];
+  p = uni(p);
+  i = uni(i);
+  const int row0 = uni(A.pass_tab[2 * p]);
+  pivot = uni(A.pass_tab[2 * p + 1]);
   ch = row0 + i;
   const float* base = A.win + (int64_t)p * A.pass_stride;
   const float* piv = base + (int64_t)pivot * A.ch_stride;
   const float* rcv = base + (int64_t)ch * A.ch_stride;
   const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
-  float2 Cf[NJ], Co[NJ];
-  nwin_f = side_spectrum<N>(piv, rcv, seg[0], seg[1], A.w, A.hop, bufA, bufB, tw, lane, Cf);
-  if (other) {
-    nwin_o = side_spectrum<N>(piv, rcv, seg[2], seg[3], A.w, A.hop, bufA, bufB, tw, lane, Co);
-  } else {
-    nwin_o = 0;
+  const int w = A.w, hop = A.hop;
+  const int a_f = uni(seg[0]), a_o = uni(seg[2]);
+  nwin_f = n_subwin(uni(seg[1]), w, hop);
+  nwin_o = other ? n_subwin(uni(seg[3]), w, hop) : 0;
+  const int nq = nwin_f + nwin_o;
+  float2 Cf[NJ], Co[NJ], z[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) Co[j] = make_float2(0.f, 0.f);
+  for (int j = 0; j < NJ; ++j) {
+    Cf[j] = make_float2(0.f, 0.f);
+    Co[j] = make_float2(0.f, 0.f);
+  }
+  if (nq > 0) load_subwin<N>(piv, rcv, nwin_f > 0 ? a_f : a_o, w, lane, z);
+  for (int q = 0; q < nq; ++q) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = lane + 64 * j;
+      if (n < N) bufA[n] = z[j];
+    }
+    if (q + 1 < nq) {
+      const int qn = q + 1;
+      const int an = qn < nwin_f ? a_f + qn * hop : a_o + (qn - nwin_f) * hop;
+      load_subwin<N>(piv, rcv, an, w, lane, z);
+    }
+    wave_sync();
+    const float2* X = FftPlan<N>::T::run(bufA, bufB, tw, lane);
+    const bool fwd = q < nwin_f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int f = lane + 64 * j;
+      if (f < N) {
+        const float2 Az = X[f];
+        const float2 Bc = X[f == 0 ? 0 : N - f];  // B = conj(Bc)
+        const float bx = Bc.x, by = -Bc.y;
+        // P = (A + B) / 2, R = (A - B) / 2i  ->  P conj(R) = (i / 4) (A + B) conj(A - B)
+        const float cx = 0.5f * (bx * Az.y - by * Az.x);
+        const float cy = 0.25f * ((Az.x * Az.x + Az.y * Az.y) - (bx * bx + by * by));
+        if (fwd) {
+          Cf[j].x += cx;
+          Cf[j].y += cy;
+        } else {
+          Co[j].x += cx;
+          Co[j].y += cy;
+        }
+      }
+    }
+    wave_sync();
   }
   // inverse FFT of W = Cf + i Co via conj(FFT(conj(W)))
 #pragma unroll
@@ -129,8 +152,7 @@ __device__ __forceinline__ const float2* row_correlations(const VsgArgs& A, int 
     if (f < N) bufA[f] = make_float2(Cf[j].x - Co[j].y, -(Cf[j].y + Co[j].x));
   }
   wave_sync();
-  const float2* Y = FftPlan<N>::T::run(bufA, bufB, tw, lane);
-  return Y;
+  return FftPlan<N>::T::run(bufA, bufB, tw, lane);
 }
 
 // c[k] (scaled by N * nwin) for the side held in component `comp` (0 -> fwd (+x), 1 -> other (-y)).
@@ -262,8 +284,8 @@ __device__ __forceinline__ void gather_row(const VsgArgs& A, const float* __rest
     ff = nwf > 0 ? 1.0f / ((float)N * (float)nwf) : 0.f;
     fo = nwo > 0 ? 1.0f / ((float)N * (float)nwo) : 0.f;
   }
-  ff *= scales[2 * p];
-  fo *= scales[2 * p + 1];
+  ff *= __builtin_bit_cast(float, uni(__builtin_bit_cast(int, scales[2 * p])));
+  fo *= __builtin_bit_cast(float, uni(__builtin_bit_cast(int, scales[2 * p + 1])));
   const bool fwd_shared = ch <= pivot;
   const bool oth_shared = ch >= pivot;
   float O[NJ];
@@ -340,16 +362,16 @@ __global__ __launch_bounds__(kBlock) void vsg_stack_kernel(VsgArgs A, const floa
   constexpr int NJ = (N + 63) / 64;
   const int64_t n_task = (int64_t)n_chunk * A.R;
   for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < n_task; t += (int64_t)gridDim.x * kWaves) {
-    const int c = (int)(t / A.R), i = (int)(t % A.R);
-    const int b = chunk_tab[3 * c], e = chunk_tab[3 * c + 1], slot = chunk_tab[3 * c + 2];
+    const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
+    const int b = uni(chunk_tab[3 * c]), e = uni(chunk_tab[3 * c + 1]), slot = uni(chunk_tab[3 * c + 2]);
     float acc[NJ];
 #pragma unroll
     for (int m = 0; m < NJ; ++m) acc[m] = 0.f;
     for (int q = b; q < e; ++q) {
-      const int p = order[q];
+      const int p = uni(order[q]);
       float G[NJ];
       gather_row<N, PAD>(A, scales, p, i, bufA, bufB, tw, lane, G);
-      const float wp = weight[p];
+      const float wp = __builtin_bit_cast(float, uni(__builtin_bit_cast(int, weight[p])));
 #pragma unroll
       for (int m = 0; m < NJ; ++m) acc[m] += G[m] * wp;
     }

@@ -11,6 +11,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#ifndef DVH_STAGE_UNROLL
+#define DVH_STAGE_UNROLL 0
+#endif
+
 namespace dvh {
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -89,7 +93,11 @@ __device__ __forceinline__ void stockham_stage(const float2* __restrict__ in, fl
   constexpr int NB = N / R;
   constexpr int TWS = N / (Ls * R);
   static_assert(N % (Ls * R) == 0, "plan does not divide N");
+#if DVH_STAGE_UNROLL
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
   for (int i0 = 0; i0 < NB; i0 += 64) {
     const int i = i0 + lane;
     if (NB % 64 == 0 || i < NB) {
