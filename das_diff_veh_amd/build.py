@@ -19,7 +19,7 @@ LIB = os.path.join(OUT_DIR, "libdvh.so")
 OBJ_DIR = os.path.join(OUT_DIR, "obj")
 ARCH = os.environ.get("DVH_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-fno-slp-vectorize",
           "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
 
 

@@ -30,142 +30,25 @@
 #include <stdint.h>
 #include <math.h>
 
-#include "fft_wave.h"
+#include "vsg_engines.h"
 #include "dvh_common.h"
 #include "dvh.h"
 
 namespace dvh {
 
-constexpr int kWaves = 4;
-constexpr int kBlock = 64 * kWaves;
-
-enum : int32_t {
-  kFlagOtherSide = 1,
-  kFlagNorm = 2,
-  kFlagNormAmp = 4,
+constexpr int kBlock = 256;  // sumsq kernel
+// waves per SIMD the kernels are compiled for: one 7-wave Eng500 block (145 KB LDS) per CU;
+// the Stockham engines are register-limited to 3
+template <class E> struct Occ { static constexpr int v = 3; };
+template <> struct Occ<Eng500> { static constexpr int v = 2; };
+#ifndef DVH_STACKF_OCC
+#define DVH_STACKF_OCC 0
+#endif
+// Occupancy target of the stack kernels: 4 waves/SIMD for the exact Stockham engines up to N = 500
+// (their spills at 128 VGPRs sit in the rare time-domain fallback only), else the engine default.
+template <class E> struct OccF {
+  static constexpr int v = DVH_STACKF_OCC ? DVH_STACKF_OCC : (E::kWaves == 4 && E::NFFT <= 500 ? 4 : Occ<E>::v);
 };
-
-struct VsgArgs {
-  const float* win;
-  int64_t pass_stride;
-  int64_t ch_stride;
-  const int32_t* pass_tab;
-  const int32_t* seg_tab;
-  int32_t n_pass;
-  int32_t R;
-  int32_t w;
-  int32_t hop;
-  int32_t flags;
-};
-
-__device__ __forceinline__ int pmod(int a, int m) {
-  const int r = a % m;
-  return r < 0 ? r + m : r;
-}
-
-__device__ __forceinline__ int n_subwin(int L, int w, int hop) { return (L >= w) ? (L - w) / hop + 1 : 0; }
-
-// Wave-uniform value (keeps table indices and table entries in SGPRs -> scalar loads).
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// Global -> register staging of one sub-window z = pivot + i * receiver (lane owns n = lane + 64 j).
-template <int N>
-__device__ __forceinline__ void load_subwin(const float* __restrict__ piv, const float* __restrict__ rcv, int a,
-                                            int w, int lane, float2 (&z)[(N + 63) / 64]) {
-  constexpr int NJ = (N + 63) / 64;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int n = lane + 64 * j;
-    z[j] = (n < w) ? make_float2(piv[a + n], rcv[a + n]) : make_float2(0.f, 0.f);
-  }
-}
-
-// Both sides of one gather row -> raw correlations in LDS: Y[k].x = N * sum_s c_f, -Y[k].y = N * sum_s c_o.
-// The sub-windows of both sides form one sequence q = 0 .. nwf + nwo - 1; the global loads of
-// sub-window q + 1 are issued before the FFT of sub-window q so their latency hides under it.
-template <int N>
-__device__ __forceinline__ const float2* row_correlations(const VsgArgs& A, int p, int i, bool other,
-                                                          float2* bufA, float2* bufB, const float2* tw,
-                                                          int lane, int& nwin_f, int& nwin_o, int& ch,
-                                                          int& pivot) {
-  constexpr int NJ = (N + 63) / 64;
-  p = uni(p);
-  i = uni(i);
-  const int row0 = uni(A.pass_tab[2 * p]);
-  pivot = uni(A.pass_tab[2 * p + 1]);
-  ch = row0 + i;
-  const float* base = A.win + (int64_t)p * A.pass_stride;
-  const float* piv = base + (int64_t)pivot * A.ch_stride;
-  const float* rcv = base + (int64_t)ch * A.ch_stride;
-  const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
-  const int w = A.w, hop = A.hop;
-  const int a_f = uni(seg[0]), a_o = uni(seg[2]);
-  nwin_f = n_subwin(uni(seg[1]), w, hop);
-  nwin_o = other ? n_subwin(uni(seg[3]), w, hop) : 0;
-  const int nq = nwin_f + nwin_o;
-  float2 Cf[NJ], Co[NJ], z[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    Cf[j] = make_float2(0.f, 0.f);
-    Co[j] = make_float2(0.f, 0.f);
-  }
-  if (nq > 0) load_subwin<N>(piv, rcv, nwin_f > 0 ? a_f : a_o, w, lane, z);
-  for (int q = 0; q < nq; ++q) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = lane + 64 * j;
-      if (n < N) bufA[n] = z[j];
-    }
-    if (q + 1 < nq) {
-      const int qn = q + 1;
-      const int an = qn < nwin_f ? a_f + qn * hop : a_o + (qn - nwin_f) * hop;
-      load_subwin<N>(piv, rcv, an, w, lane, z);
-    }
-    wave_sync();
-    const float2* X = FftPlan<N>::T::run(bufA, bufB, tw, lane);
-    const bool fwd = q < nwin_f;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int f = lane + 64 * j;
-      if (f < N) {
-        const float2 Az = X[f];
-        const float2 Bc = X[f == 0 ? 0 : N - f];  // B = conj(Bc)
-        const float bx = Bc.x, by = -Bc.y;
-        // P = (A + B) / 2, R = (A - B) / 2i  ->  P conj(R) = (i / 4) (A + B) conj(A - B)
-        const float cx = 0.5f * (bx * Az.y - by * Az.x);
-        const float cy = 0.25f * ((Az.x * Az.x + Az.y * Az.y) - (bx * bx + by * by));
-        if (fwd) {
-          Cf[j].x += cx;
-          Cf[j].y += cy;
-        } else {
-          Co[j].x += cx;
-          Co[j].y += cy;
-        }
-      }
-    }
-    wave_sync();
-  }
-  // inverse FFT of W = Cf + i Co via conj(FFT(conj(W)))
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int f = lane + 64 * j;
-    if (f < N) bufA[f] = make_float2(Cf[j].x - Co[j].y, -(Cf[j].y + Co[j].x));
-  }
-  wave_sync();
-  return FftPlan<N>::T::run(bufA, bufB, tw, lane);
-}
-
-// c[k] (scaled by N * nwin) for the side held in component `comp` (0 -> fwd (+x), 1 -> other (-y)).
-template <int N, bool PAD>
-__device__ __forceinline__ float2 read_c(const float2* Y, int k, int w) {
-  float2 v = Y[k];
-  if (PAD && k > 0) {
-    const float2 u = Y[N - w + k];
-    v.x += u.x;
-    v.y += u.y;
-  }
-  return make_float2(v.x, -v.y);
-}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -179,24 +62,28 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+template <class E>
+__device__ __forceinline__ E make_engine(char* lds) {
+  E::block_init(lds);
+  __syncthreads();
+  return E(lds, threadIdx.x >> 6, threadIdx.x & 63);
+}
+
 // Per-pass scale of each side: 1 / max(pivot autocorrelation row) after the optional row norm
 // (post_processing_XCF with norm_amp=True); 1 / ||window||_F^2 when neither norm is requested.
-template <int N, bool PAD>
-__global__ __launch_bounds__(kBlock) void vsg_scales_kernel(VsgArgs A, const double* __restrict__ sumsq,
+template <class E>
+__global__ __launch_bounds__(64 * E::kWaves, Occ<E>::v) void vsg_scales_kernel(VsgArgs A, const double* __restrict__ sumsq,
                                                              float* __restrict__ scales) {
-  extern __shared__ __attribute__((aligned(16))) float2 smem[];
-  float2* tw = smem;
-  init_twiddles<N>(tw);
-  __syncthreads();
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  E eng = make_engine<E>(lds);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  float2* bufA = smem + N + wave * 2 * N;
-  float2* bufB = bufA + N;
   const bool other = (A.flags & kFlagOtherSide) != 0;
   const bool norm = (A.flags & kFlagNorm) != 0;
   const bool norm_amp = (A.flags & kFlagNormAmp) != 0;
-  constexpr int NJ = (N + 63) / 64;
-  for (int p = blockIdx.x * kWaves + wave; p < A.n_pass; p += gridDim.x * kWaves) {
+  constexpr int NJ = E::NJ;
+  const int stride = gridDim.x * E::kWaves;
+  for (int p = blockIdx.x * E::kWaves + wave; p < A.n_pass; p += stride) {
     if (!norm_amp) {
       if (lane == 0) {
         const float s = norm ? 1.0f : (float)(1.0 / sumsq[p]);
@@ -205,19 +92,21 @@ __global__ __launch_bounds__(kBlock) void vsg_scales_kernel(VsgArgs A, const dou
       }
       continue;
     }
-    const int i = A.pass_tab[2 * p + 1] - A.pass_tab[2 * p];  // pivot row of the gather
-    int nwf, nwo, ch, pivot;
-    const float2* Y = row_correlations<N>(A, p, i, other, bufA, bufB, tw, lane, nwf, nwo, ch, pivot);
+    const RowTask t = make_task(A, p, uni(A.pass_tab[2 * p + 1] - A.pass_tab[2 * p]));  // the pivot row
+    RowTask tn = t;
+    const bool has_next = norm_amp && p + stride < A.n_pass;
+    if (has_next) tn = make_task(A, p + stride, uni(A.pass_tab[2 * (p + stride) + 1] - A.pass_tab[2 * (p + stride)]));
+    const float2* Y = eng.correlate(t, tn, has_next, A.w, A.hop);
     float mf = -INFINITY, mo = -INFINITY, sf = 0.f, so = 0.f;
     bool nanf = false, nano = false;
-    // a side with no sub-window is exactly zero in the reference (the packed inverse FFT would
-    // otherwise leak the other side's rounding into it)
-    const float2 live = make_float2(nwf > 0 ? 1.f : 0.f, nwo > 0 ? 1.f : 0.f);
+    // a side with nothing accumulated is exactly zero in the reference (the packed inverse FFT
+    // would otherwise leak the other side's rounding into it)
+    const float2 live = make_float2(eng.live_f ? 1.f : 0.f, eng.live_o ? 1.f : 0.f);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int k = lane + 64 * j;
       if (k < A.w) {
-        float2 c = read_c<N, PAD>(Y, k, A.w);
+        float2 c = eng.c(Y, k, A.w);
         c.x *= live.x;
         c.y *= live.y;
         nanf |= isnan(c.x);
@@ -239,8 +128,8 @@ __global__ __launch_bounds__(kBlock) void vsg_scales_kernel(VsgArgs A, const dou
       amax_f = mf / sqrtf(sf);
       amax_o = mo / sqrtf(so);
     } else {
-      amax_f = nwf > 0 ? mf / ((float)N * (float)nwf) : 0.f;
-      amax_o = nwo > 0 ? mo / ((float)N * (float)nwo) : 0.f;
+      amax_f = t.nwin_f > 0 ? mf / ((float)E::NFFT * (float)t.nwin_f) : 0.f;
+      amax_o = t.nwin_o > 0 ? mo / ((float)E::NFFT * (float)t.nwin_o) : 0.f;
     }
     if (anynanf) amax_f = NAN;
     if (anynano) amax_o = NAN;
@@ -251,43 +140,54 @@ __global__ __launch_bounds__(kBlock) void vsg_scales_kernel(VsgArgs A, const dou
   }
 }
 
-// Final gather row for (pass p, row i): G[m] for j = lane + 64 m.
-template <int N, bool PAD>
-__device__ __forceinline__ void gather_row(const VsgArgs& A, const float* __restrict__ scales, int p, int i,
-                                           float2* bufA, float2* bufB, const float2* tw, int lane,
-                                           float (&G)[(N + 63) / 64]) {
-  constexpr int NJ = (N + 63) / 64;
+// Applies the per-pass scales to the row factors.  With neither norm the reference scales the DATA
+// (data / ||data||, virtual_shot_gather.py:124), so a side without sub-windows stays exactly 0 even
+// when the window is all zero or holds a NaN; otherwise the scale divides the finished row and
+// 0 * (1 / amax) reproduces its 0 / amax.
+__device__ __forceinline__ void side_scale(int flags, const RowTask& t, float sf, float so, float& ff, float& fo) {
+  if (!(flags & (kFlagNorm | kFlagNormAmp))) {
+    ff = t.nwin_f > 0 ? ff * sf : 0.f;
+    fo = t.nwin_o > 0 ? fo * so : 0.f;
+  } else {
+    ff *= sf;
+    fo *= so;
+  }
+}
+
+// Time-domain epilogue of a row: lag permutation, per-pass scales, optional row norm, two-sided
+// average -> G[m] for output lag j = lane + 64 m (post_processing_XCF + VirtualShotGather.__init__).
+template <class E>
+__device__ __forceinline__ void row_epilogue(const E& eng, const VsgArgs& A, const float2* Y, const RowTask& t,
+                                             float sf, float so, int lane, float (&G)[E::NJ]) {
+  constexpr int NJ = E::NJ;
   const bool other = (A.flags & kFlagOtherSide) != 0;
   const bool norm = (A.flags & kFlagNorm) != 0;
-  int nwf, nwo, ch, pivot;
-  const float2* Y = row_correlations<N>(A, p, i, other, bufA, bufB, tw, lane, nwf, nwo, ch, pivot);
   const int w = A.w, h = w / 2;
-  // a side with no sub-window is exactly zero in the reference (see vsg_scales_kernel)
-  const float2 live = make_float2(nwf > 0 ? 1.f : 0.f, nwo > 0 ? 1.f : 0.f);
+  // a side with nothing accumulated is exactly zero in the reference (see vsg_scales_kernel)
+  const float2 live = make_float2(eng.live_f ? 1.f : 0.f, eng.live_o ? 1.f : 0.f);
   float ff, fo;
   if (norm) {
-    float sf = 0.f, so = 0.f;
+    float s2f = 0.f, s2o = 0.f;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int k = lane + 64 * j;
       if (k < w) {
-        float2 c = read_c<N, PAD>(Y, k, w);
+        float2 c = eng.c(Y, k, w);
         c.x *= live.x;
         c.y *= live.y;
-        sf += c.x * c.x;
-        so += c.y * c.y;
+        s2f += c.x * c.x;
+        s2o += c.y * c.y;
       }
     }
-    ff = 1.0f / sqrtf(wave_sum(sf));
-    fo = 1.0f / sqrtf(wave_sum(so));
+    ff = 1.0f / sqrtf(wave_sum(s2f));
+    fo = 1.0f / sqrtf(wave_sum(s2o));
   } else {
-    ff = nwf > 0 ? 1.0f / ((float)N * (float)nwf) : 0.f;
-    fo = nwo > 0 ? 1.0f / ((float)N * (float)nwo) : 0.f;
+    ff = t.nwin_f > 0 ? 1.0f / ((float)E::NFFT * (float)t.nwin_f) : 0.f;
+    fo = t.nwin_o > 0 ? 1.0f / ((float)E::NFFT * (float)t.nwin_o) : 0.f;
   }
-  ff *= __builtin_bit_cast(float, uni(__builtin_bit_cast(int, scales[2 * p])));
-  fo *= __builtin_bit_cast(float, uni(__builtin_bit_cast(int, scales[2 * p + 1])));
-  const bool fwd_shared = ch <= pivot;
-  const bool oth_shared = ch >= pivot;
+  side_scale(A.flags, t, sf, so, ff, fo);
+  const bool fwd_shared = t.ch <= t.pivot;
+  const bool oth_shared = t.ch >= t.pivot;
   float O[NJ];
   bool nan_o = false, nz_o = false;
 #pragma unroll
@@ -297,10 +197,10 @@ __device__ __forceinline__ void gather_row(const VsgArgs& A, const float* __rest
     O[m] = 0.f;
     if (j < w) {
       const int kf = fwd_shared ? pmod(w - 1 - j - h, w) : pmod(j + h + 1, w);
-      G[m] = (read_c<N, PAD>(Y, kf, w).x * live.x) * ff;
+      G[m] = (eng.c(Y, kf, w).x * live.x) * ff;
       if (other) {
         const int ko = oth_shared ? pmod(h - 1 - j, w) : pmod(j - h, w);
-        O[m] = (read_c<N, PAD>(Y, ko, w).y * live.y) * fo;
+        O[m] = (eng.c(Y, ko, w).y * live.y) * fo;
         nan_o |= isnan(O[m]);
         nz_o |= (O[m] != 0.f);
       }
@@ -317,23 +217,32 @@ __device__ __forceinline__ void gather_row(const VsgArgs& A, const float* __rest
   }
 }
 
-template <int N, bool PAD>
-__global__ __launch_bounds__(kBlock) void vsg_gather_kernel(VsgArgs A, const float* __restrict__ scales,
+template <class E>
+__device__ __forceinline__ void gather_row(E& eng, const VsgArgs& A, const float* __restrict__ scales, int p,
+                                           const RowTask& t, const RowTask& nt, bool has_next, int lane,
+                                           float (&G)[E::NJ]) {
+  const float2* Y = eng.correlate(t, nt, has_next, A.w, A.hop);
+  row_epilogue<E>(eng, A, Y, t, unif(scales[2 * p]), unif(scales[2 * p + 1]), lane, G);
+}
+
+template <class E>
+__global__ __launch_bounds__(64 * E::kWaves, Occ<E>::v) void vsg_gather_kernel(VsgArgs A, const float* __restrict__ scales,
                                                              float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float2 smem[];
-  float2* tw = smem;
-  init_twiddles<N>(tw);
-  __syncthreads();
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  E eng = make_engine<E>(lds);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  float2* bufA = smem + N + wave * 2 * N;
-  float2* bufB = bufA + N;
-  constexpr int NJ = (N + 63) / 64;
+  constexpr int NJ = E::NJ;
   const int64_t n_task = (int64_t)A.n_pass * A.R;
-  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < n_task; t += (int64_t)gridDim.x * kWaves) {
-    const int p = (int)(t / A.R), i = (int)(t % A.R);
+  const int64_t stride = (int64_t)gridDim.x * E::kWaves;
+  for (int64_t t = (int64_t)blockIdx.x * E::kWaves + wave; t < n_task; t += stride) {
+    const int p = uni((int)(t / A.R)), i = uni((int)(t % A.R));
+    const RowTask task = make_task(A, p, i);
+    RowTask tn = task;
+    const bool has_next = t + stride < n_task;
+    if (has_next) tn = make_task(A, (int)((t + stride) / A.R), (int)((t + stride) % A.R));
     float G[NJ];
-    gather_row<N, PAD>(A, scales, p, i, bufA, bufB, tw, lane, G);
+    gather_row<E>(eng, A, scales, p, task, tn, has_next, lane, G);
     float* o = out + t * A.w;
 #pragma unroll
     for (int m = 0; m < NJ; ++m) {
@@ -345,35 +254,46 @@ __global__ __launch_bounds__(kBlock) void vsg_gather_kernel(VsgArgs A, const flo
 
 // Stack mode: task = (chunk c, row i); the wave walks the chunk's passes (all of one class slot),
 // sums weight[p] * G_p in registers and adds the row into stack[slot] once.
-template <int N, bool PAD>
-__global__ __launch_bounds__(kBlock) void vsg_stack_kernel(VsgArgs A, const float* __restrict__ scales,
+template <class E>
+__global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stack_kernel(VsgArgs A, const float* __restrict__ scales,
                                                             const int32_t* __restrict__ order,
                                                             const int32_t* __restrict__ chunk_tab, int32_t n_chunk,
                                                             const float* __restrict__ weight,
                                                             float* __restrict__ stack) {
-  extern __shared__ __attribute__((aligned(16))) float2 smem[];
-  float2* tw = smem;
-  init_twiddles<N>(tw);
-  __syncthreads();
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  E eng = make_engine<E>(lds);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  float2* bufA = smem + N + wave * 2 * N;
-  float2* bufB = bufA + N;
-  constexpr int NJ = (N + 63) / 64;
+  constexpr int NJ = E::NJ;
   const int64_t n_task = (int64_t)n_chunk * A.R;
-  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave; t < n_task; t += (int64_t)gridDim.x * kWaves) {
+  const int64_t stride = (int64_t)gridDim.x * E::kWaves;
+  for (int64_t t = (int64_t)blockIdx.x * E::kWaves + wave; t < n_task; t += stride) {
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = uni(chunk_tab[3 * c]), e = uni(chunk_tab[3 * c + 1]), slot = uni(chunk_tab[3 * c + 2]);
+    // first pass of the wave's next task (for the cross-task slice prefetch)
+    int np = -1, ni = 0;
+    if (t + stride < n_task) {
+      const int c2 = uni((int)((t + stride) / A.R));
+      ni = uni((int)((t + stride) % A.R));
+      const int b2 = uni(chunk_tab[3 * c2]);
+      if (b2 < uni(chunk_tab[3 * c2 + 1])) np = uni(order[b2]);
+    }
     float acc[NJ];
 #pragma unroll
     for (int m = 0; m < NJ; ++m) acc[m] = 0.f;
+    RowTask task = b < e ? make_task(A, uni(order[b]), i) : RowTask{};
     for (int q = b; q < e; ++q) {
       const int p = uni(order[q]);
+      RowTask tn = task;
+      const bool has_next = (q + 1 < e) || np >= 0;
+      if (q + 1 < e) tn = make_task(A, uni(order[q + 1]), i);
+      else if (np >= 0) tn = make_task(A, np, ni);
       float G[NJ];
-      gather_row<N, PAD>(A, scales, p, i, bufA, bufB, tw, lane, G);
-      const float wp = __builtin_bit_cast(float, uni(__builtin_bit_cast(int, weight[p])));
+      gather_row<E>(eng, A, scales, p, task, tn, has_next, lane, G);
+      const float wp = unif(weight[p]);
 #pragma unroll
       for (int m = 0; m < NJ; ++m) acc[m] += G[m] * wp;
+      task = tn;
     }
     float* o = stack + ((int64_t)slot * A.R + i) * A.w;
 #pragma unroll
@@ -384,11 +304,139 @@ __global__ __launch_bounds__(kBlock) void vsg_stack_kernel(VsgArgs A, const floa
   }
 }
 
+// Stack mode, exact transforms (N == w): every pass's contribution is accumulated directly as the
+// spectrum of its output row, Ghat[m] += w_p (alpha f_f Phase_F(Cf) + beta f_o Phase_O(Co)), where
+// each lag convention of the reference is a conjugation and a phase ramp:
+//   c[(a - j) mod w]  ->  W^(a m) conj(C[m]),      c[(j + b) mod w]  ->  W^(-b m) C[m]
+// (alpha, beta) = (1/2, 1/2) when the other side is finite and non-zero, else (1, 0).  One inverse
+// transform per (chunk, row) replaces the per-pass inverse transform and epilogue.  Passes with a
+// non-finite scale or NaN data go through the exact time-domain path (row_epilogue) instead.
+template <class E>
+__global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
+    VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
+    const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
+    float* __restrict__ stack) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  E eng = make_engine<E>(lds);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  constexpr int NJ = E::NJ;
+  constexpr int NH = E::NH;
+  constexpr int N = E::NFFT;
+  const bool other = (A.flags & kFlagOtherSide) != 0;
+  const bool norm = (A.flags & kFlagNorm) != 0;
+  const int h = N / 2;
+  const int64_t n_task = (int64_t)n_chunk * A.R;
+  const int64_t stride = (int64_t)gridDim.x * E::kWaves;
+  for (int64_t t = (int64_t)blockIdx.x * E::kWaves + wave; t < n_task; t += stride) {
+    const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
+    const int b = uni(chunk_tab[3 * c]), e = uni(chunk_tab[3 * c + 1]), slot = uni(chunk_tab[3 * c + 2]);
+    int np = -1, ni = 0;
+    if (t + stride < n_task) {
+      const int c2 = uni((int)((t + stride) / A.R));
+      ni = uni((int)((t + stride) % A.R));
+      const int b2 = uni(chunk_tab[3 * c2]);
+      if (b2 < uni(chunk_tab[3 * c2 + 1])) np = uni(order[b2]);
+    }
+    float* o = stack + ((int64_t)slot * A.R + i) * A.w;
+    float2 Gh[NH];
+#pragma unroll
+    for (int m = 0; m < NH; ++m) Gh[m] = make_float2(0.f, 0.f);
+    RowTask task = b < e ? make_task(A, uni(order[b]), i) : RowTask{};
+    for (int q = b; q < e; ++q) {
+      const int p = uni(order[q]);
+      RowTask tn = task;
+      const bool has_next = (q + 1 < e) || np >= 0;
+      if (q + 1 < e) tn = make_task(A, uni(order[q + 1]), i);
+      else if (np >= 0) tn = make_task(A, np, ni);
+      float2 Cf[NH], Co[NH];
+      eng.spectra(task, tn, has_next, A.w, A.hop, Cf, Co);
+      const float sf = unif(scales[2 * p]), so = unif(scales[2 * p + 1]), wp = unif(weight[p]);
+      bool bad = false, nzo = false;
+      float s2f = 0.f, s2o = 0.f;
+#pragma unroll
+      for (int m = 0; m < NH; ++m) {
+        const int f = lane + 64 * m;
+        if (f <= h) {
+          bad |= isnan(Cf[m].x) || isnan(Cf[m].y) || isnan(Co[m].x) || isnan(Co[m].y);
+          nzo |= (Co[m].x != 0.f) || (Co[m].y != 0.f);
+          // Parseval over all N bins from the half spectrum: interior bins count twice
+          const float wgt = (f == 0 || f == h) ? 1.f : 2.f;
+          s2f += wgt * (Cf[m].x * Cf[m].x + Cf[m].y * Cf[m].y);
+          s2o += wgt * (Co[m].x * Co[m].x + Co[m].y * Co[m].y);
+        }
+      }
+      bad = __ballot(bad) != 0;
+      nzo = other && (__ballot(nzo) != 0);
+      float ff, fo;
+      if (norm) {  // ||c||^2 = sum_m |C[m]|^2 / N
+        ff = sqrtf((float)N) / sqrtf(wave_sum(s2f));
+        fo = sqrtf((float)N) / sqrtf(wave_sum(s2o));
+      } else {
+        ff = task.nwin_f > 0 ? 1.0f / (float)task.nwin_f : 0.f;
+        fo = task.nwin_o > 0 ? 1.0f / (float)task.nwin_o : 0.f;
+      }
+      side_scale(A.flags, task, sf, so, ff, fo);
+      if (bad || !isfinite(ff) || (nzo && !isfinite(fo))) {
+        // exact time-domain path (NaN / inf semantics of the reference), added straight to the stack
+        const float2* Y = eng.inverse(Cf, Co);
+        float G[NJ];
+        row_epilogue<E>(eng, A, Y, task, sf, so, lane, G);
+#pragma unroll
+        for (int m = 0; m < NJ; ++m) {
+          const int j = lane + 64 * m;
+          if (j < A.w) atomicAdd(o + j, G[m] * wp);
+        }
+        wave_sync();
+      } else {
+        // other row finite and not identically zero (row_epilogue's test)
+        const bool ok = nzo && fo != 0.f;
+        const float cf = wp * (ok ? 0.5f : 1.f) * ff;
+        const float co = ok ? wp * 0.5f * fo : 0.f;
+        const bool fwd_shared = task.ch <= task.pivot;
+        const bool oth_shared = task.ch >= task.pivot;
+        // W^(s m): fwd shared s = w-1-h (conj), fwd traj s = -(h+1); other shared s = h-1 (conj),
+        // other traj s = h
+        const int sf_shift = fwd_shared ? N - 1 - h : N - (h + 1);
+        const int so_shift = oth_shared ? h - 1 : h;
+#pragma unroll
+        for (int m = 0; m < NH; ++m) {
+          const int f = lane + 64 * m;
+          if (f <= h) {
+            float2 x = fwd_shared ? make_float2(Cf[m].x, -Cf[m].y) : Cf[m];
+            x = cmul(x, eng.twiddle((sf_shift * f) % N));
+            Gh[m].x += cf * x.x;
+            Gh[m].y += cf * x.y;
+            if (ok) {
+              float2 y = oth_shared ? make_float2(Co[m].x, -Co[m].y) : Co[m];
+              y = cmul(y, eng.twiddle((so_shift * f) % N));
+              Gh[m].x += co * y.x;
+              Gh[m].y += co * y.y;
+            }
+          }
+        }
+      }
+      task = tn;
+    }
+    float2 Z[NH];
+#pragma unroll
+    for (int m = 0; m < NH; ++m) Z[m] = make_float2(0.f, 0.f);
+    const float2* Y = eng.inverse(Gh, Z);
+    const float inv_n = 1.0f / (float)N;
+#pragma unroll
+    for (int m = 0; m < NJ; ++m) {
+      const int j = lane + 64 * m;
+      if (j < A.w) atomicAdd(o + j, eng.c(Y, j, A.w).x * inv_n);
+    }
+    wave_sync();
+  }
+}
+
 // Sum of squares of each pass window (np.linalg.norm(window.data) ** 2), for norm=norm_amp=False.
 __global__ __launch_bounds__(kBlock) void window_sumsq_kernel(const float* __restrict__ win, int64_t pass_stride,
                                                                int64_t ch_stride, int32_t n_ch, int32_t n_t,
                                                                double* __restrict__ out) {
-  __shared__ double part[kWaves];
+  __shared__ double part[kBlock / 64];
   const int p = blockIdx.x;
   const float* base = win + (int64_t)p * pass_stride;
   double s = 0.0;
@@ -405,14 +453,9 @@ __global__ __launch_bounds__(kBlock) void window_sumsq_kernel(const float* __res
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
-    for (int k = 0; k < kWaves; ++k) t += part[k];
+    for (int k = 0; k < kBlock / 64; ++k) t += part[k];
     out[p] = t;
   }
-}
-
-template <int N>
-constexpr size_t vsg_lds_bytes() {
-  return sizeof(float2) * (size_t)N * (1 + 2 * kWaves);
 }
 
 struct VsgKernels {
@@ -420,12 +463,18 @@ struct VsgKernels {
   const void* gather;
   const void* stack;
   size_t lds;
+  int waves;
 };
 
-template <int N, bool PAD>
+#ifndef DVH_FREQ_STACK
+#define DVH_FREQ_STACK 1
+#endif
+
+template <class E, bool EXACT>
 VsgKernels vsg_kernels() {
-  return VsgKernels{(const void*)vsg_scales_kernel<N, PAD>, (const void*)vsg_gather_kernel<N, PAD>,
-                    (const void*)vsg_stack_kernel<N, PAD>, vsg_lds_bytes<N>()};
+  const void* st = (EXACT && DVH_FREQ_STACK) ? (const void*)vsg_stackf_kernel<E> : (const void*)vsg_stack_kernel<E>;
+  return VsgKernels{(const void*)vsg_scales_kernel<E>, (const void*)vsg_gather_kernel<E>, st,
+                    E::kBlockBytes + E::kWaves * E::kWaveBytes, E::kWaves};
 }
 
 // Transform length for a window length w: exact mixed-radix when available, else a zero-padded
@@ -440,17 +489,23 @@ static int choose_fft(int w, bool* pad) {
   return 0;
 }
 
+#ifndef DVH_VSG500
+#define DVH_VSG500 0
+#endif
+
 static bool get_kernels(int w, VsgKernels* k, int* n_out) {
   bool pad;
   const int n = choose_fft(w, &pad);
   *n_out = n;
   switch (n) {
-    case 250: *k = vsg_kernels<250, false>(); return true;
-    case 500: *k = vsg_kernels<500, false>(); return true;
-    case 1000: *k = vsg_kernels<1000, false>(); return true;
-    case 512: *k = vsg_kernels<512, true>(); return true;
-    case 1024: *k = vsg_kernels<1024, true>(); return true;
-    case 2048: *k = vsg_kernels<2048, true>(); return true;
+    case 250: *k = vsg_kernels<EngStockham<250, false>, true>(); return true;
+    case 500:
+      *k = DVH_VSG500 ? vsg_kernels<Eng500, true>() : vsg_kernels<EngStockham<500, false>, true>();
+      return true;
+    case 1000: *k = vsg_kernels<EngStockham<1000, false>, true>(); return true;
+    case 512: *k = vsg_kernels<EngStockham<512, true>, false>(); return true;
+    case 1024: *k = vsg_kernels<EngStockham<1024, true>, false>(); return true;
+    case 2048: *k = vsg_kernels<EngStockham<2048, true>, false>(); return true;
     default: return false;
   }
 }
@@ -461,11 +516,11 @@ static int check_common(const VsgArgs& A) {
   return 0;
 }
 
-static int launch(const void* fn, int grid, size_t lds, void** args, hipStream_t s) {
+static int launch(const void* fn, int grid, int waves, size_t lds, void** args, hipStream_t s) {
   if (grid <= 0) return 0;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
-  e = hipLaunchKernel(fn, dim3(grid), dim3(kBlock), args, lds, s);
+  e = hipLaunchKernel(fn, dim3(grid), dim3(64 * waves), args, lds, s);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
   return 0;
 }
@@ -501,7 +556,7 @@ DVH_API int dvh_vsg_scales(const float* win, int64_t pass_stride, int64_t ch_str
   int n;
   if (!get_kernels(w, &k, &n)) return set_error(-4, "unsupported correlation window length");
   void* args[] = {&A, &win_sumsq, &scales};
-  return launch(k.scales, (n_pass + kWaves - 1) / kWaves, k.lds, args, (hipStream_t)stream);
+  return launch(k.scales, (n_pass + k.waves - 1) / k.waves, k.waves, k.lds, args, (hipStream_t)stream);
 }
 
 DVH_API int dvh_vsg_gathers(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass,
@@ -514,9 +569,9 @@ DVH_API int dvh_vsg_gathers(const float* win, int64_t pass_stride, int64_t ch_st
   int n;
   if (!get_kernels(w, &k, &n)) return set_error(-4, "unsupported correlation window length");
   const int64_t tasks = (int64_t)n_pass * R;
-  const int64_t grid = (tasks + kWaves - 1) / kWaves;
+  const int64_t grid = (tasks + k.waves - 1) / k.waves;
   void* args[] = {&A, &scales, &out};
-  return launch(k.gather, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.lds, args, (hipStream_t)stream);
+  return launch(k.gather, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, (hipStream_t)stream);
 }
 
 DVH_API int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass,
@@ -530,7 +585,7 @@ DVH_API int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stri
   int n;
   if (!get_kernels(w, &k, &n)) return set_error(-4, "unsupported correlation window length");
   const int64_t tasks = (int64_t)n_chunk * R;
-  const int64_t grid = (tasks + kWaves - 1) / kWaves;
+  const int64_t grid = (tasks + k.waves - 1) / k.waves;
   void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack};
-  return launch(k.stack, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.lds, args, (hipStream_t)stream);
+  return launch(k.stack, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, (hipStream_t)stream);
 }

@@ -1,0 +1,515 @@
+// Per-wave correlation engines of the VSG kernels (gfx950).
+//
+// An engine turns one gather row task (pass p, row i) into the raw circular correlations of both
+// sides, c_f[k] and c_o[k] (k < w), summed over the row's sub-windows and scaled by N * nwin:
+//   for every sub-window, z = pivot + i * receiver -> one complex FFT -> cross spectrum
+//   P conj(R) = (i/4)(Z[f] + conj Z[-f]) conj(Z[f] - conj Z[-f]) accumulated per side in registers,
+//   then ONE inverse FFT of Cf + i Co (real part -> forward side, imaginary -> other side).
+// The cross spectra of real correlations are Hermitian, so only bins f <= N/2 are accumulated
+// (NH per lane, f = lane + 64 j); the inverse writes both W[f] and W[N - f].
+// A sub-window whose pivot or receiver slice is identically zero contributes exactly zero in the
+// reference; the engines test every loaded sample (bit pattern, so NaN counts as non-zero) and skip
+// such sub-windows, and report per side whether anything was accumulated (live_f / live_o), so that
+// an all-zero side is exactly zero (and yields the reference's 0/0 = NaN where it normalises).
+//
+//   EngStockham<N, PAD>  any supported N: LDS ping-pong Stockham transform (fft_wave.h), sub-window
+//                        loads staged in registers one sub-window ahead.  PAD: N >= 2w - 1 zero padded,
+//                        linear correlation folded back to circular in c().
+//   Eng500               N = w = 500 (wlen = 2 s at 250 Hz, the reference's operating point):
+//                        two-stage 20 x 25 transform with the radix-20 / radix-25 butterflies held in
+//                        registers, the three sub-windows of a side transformed together (75 + 60 lane
+//                        tasks, one LDS round trip), the side's time slice staged into LDS by
+//                        asynchronous LDS-DMA (global_load_lds_dword) issued one slice ahead -- across
+//                        sides and across consecutive tasks of the wave.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fft_wave.h"
+#include "tw_tables.h"
+
+namespace dvh {
+
+enum : int32_t {
+  kFlagOtherSide = 1,
+  kFlagNorm = 2,
+  kFlagNormAmp = 4,
+};
+
+struct VsgArgs {
+  const float* win;
+  int64_t pass_stride;
+  int64_t ch_stride;
+  const int32_t* pass_tab;
+  const int32_t* seg_tab;
+  int32_t n_pass;
+  int32_t R;
+  int32_t w;
+  int32_t hop;
+  int32_t flags;
+};
+
+__device__ __forceinline__ int pmod(int a, int m) {
+  const int r = a % m;
+  return r < 0 ? r + m : r;
+}
+
+__device__ __forceinline__ int n_subwin(int L, int w, int hop) { return (L >= w) ? (L - w) / hop + 1 : 0; }
+
+// Wave-uniform value (keeps table indices and table entries in SGPRs -> scalar loads).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float unif(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
+// Everything a row task needs, wave-uniform.
+struct RowTask {
+  const float* piv;
+  const float* rcv;
+  int a_f, nwin_f, a_o, nwin_o;
+  int ch, pivot;
+};
+
+__device__ __forceinline__ RowTask make_task(const VsgArgs& A, int p, int i) {
+  p = uni(p);
+  i = uni(i);
+  RowTask t;
+  const int row0 = uni(A.pass_tab[2 * p]);
+  t.pivot = uni(A.pass_tab[2 * p + 1]);
+  t.ch = row0 + i;
+  const float* base = A.win + (int64_t)p * A.pass_stride;
+  t.piv = base + (int64_t)t.pivot * A.ch_stride;
+  t.rcv = base + (int64_t)t.ch * A.ch_stride;
+  const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
+  t.a_f = uni(seg[0]);
+  t.nwin_f = n_subwin(uni(seg[1]), A.w, A.hop);
+  const bool other = (A.flags & kFlagOtherSide) != 0;
+  t.a_o = uni(seg[2]);
+  t.nwin_o = other ? n_subwin(uni(seg[3]), A.w, A.hop) : 0;
+  return t;
+}
+
+// |x| != 0 as a bit mask (NaN included); OR-accumulate, test once per sub-window
+__device__ __forceinline__ uint32_t nzbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
+
+__device__ __forceinline__ void accumulate_cross(float2 Az, float2 Bc, float2& C) {
+  // P = (A + B) / 2, R = (A - B) / 2i with B = conj(Bc)  ->  P conj(R) = (i / 4) (A + B) conj(A - B)
+  const float bx = Bc.x, by = -Bc.y;
+  C.x += 0.5f * (bx * Az.y - by * Az.x);
+  C.y += 0.25f * ((Az.x * Az.x + Az.y * Az.y) - (bx * bx + by * by));
+}
+
+// conj(W) for W = Cf + i Co over all N bins from the half spectra (bins f <= N/2): the input of the
+// inverse transform conj(FFT(conj(W))).  W[N - f] = conj(Cf[f]) + i conj(Co[f]).
+template <int N, int NH, class Idx>
+__device__ __forceinline__ void store_conj_hermitian(float2* buf, const float2 (&Cf)[NH], const float2 (&Co)[NH],
+                                                     int lane, Idx idx) {
+#pragma unroll
+  for (int j = 0; j < NH; ++j) {
+    const int f = lane + 64 * j;
+    if (f <= N / 2) {
+      buf[idx(f)] = make_float2(Cf[j].x - Co[j].y, -(Cf[j].y + Co[j].x));
+      if (f > 0 && f < N / 2) buf[idx(N - f)] = make_float2(Cf[j].x + Co[j].y, Cf[j].y - Co[j].x);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+template <int N, bool PAD>
+struct EngStockham {
+  static constexpr int NFFT = N;
+  static constexpr int kWaves = 4;
+  static constexpr int NJ = (N + 63) / 64;
+  static constexpr int NH = (N / 2 + 1 + 63) / 64;
+  static_assert(N % 2 == 0, "Hermitian half spectra assume an even length");
+  static constexpr size_t kBlockBytes = sizeof(float2) * N;        // twiddle table
+  static constexpr size_t kWaveBytes = sizeof(float2) * 2 * N;     // ping-pong buffers
+  float2* tw;
+  float2* bufA;
+  float2* bufB;
+  int lane;
+  bool live_f, live_o;  // some sub-window of the side had non-zero pivot and receiver slices
+
+  __device__ EngStockham(char* lds, int wave, int lane_) : lane(lane_), live_f(false), live_o(false) {
+    tw = reinterpret_cast<float2*>(lds);
+    bufA = reinterpret_cast<float2*>(lds + kBlockBytes + (size_t)wave * kWaveBytes);
+    bufB = bufA + N;
+  }
+  static __device__ void block_init(char* lds) { init_twiddles<N>(reinterpret_cast<float2*>(lds)); }
+
+  __device__ void load(const RowTask& t, int a, int w, float2 (&z)[NJ]) const {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = lane + 64 * j;
+      z[j] = (n < w) ? make_float2(t.piv[a + n], t.rcv[a + n]) : make_float2(0.f, 0.f);
+    }
+  }
+
+  // accumulated cross spectra of both sides: Cf[j], Co[j] at bins f = lane + 64 j
+  __device__ void spectra(const RowTask& t, const RowTask&, bool, int w, int hop, float2 (&Cf)[NH],
+                          float2 (&Co)[NH]) {
+    const int nq = t.nwin_f + t.nwin_o;
+    float2 z[NJ];
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      Cf[j] = make_float2(0.f, 0.f);
+      Co[j] = make_float2(0.f, 0.f);
+    }
+    live_f = live_o = false;
+    if (nq > 0) load(t, t.nwin_f > 0 ? t.a_f : t.a_o, w, z);
+    for (int q = 0; q < nq; ++q) {
+      uint32_t bp = 0, br = 0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = lane + 64 * j;
+        if (n < N) bufA[n] = z[j];
+        bp |= nzbits(z[j].x);
+        br |= nzbits(z[j].y);
+      }
+      const bool live = (__ballot(bp != 0) != 0) && (__ballot(br != 0) != 0);
+      if (q + 1 < nq) {
+        const int qn = q + 1;
+        load(t, qn < t.nwin_f ? t.a_f + qn * hop : t.a_o + (qn - t.nwin_f) * hop, w, z);
+      }
+      if (!live) continue;  // exactly zero in the reference
+      if (q < t.nwin_f) live_f = true;
+      else live_o = true;
+      wave_sync();
+      const float2* X = FftPlan<N>::T::run(bufA, bufB, tw, lane);
+      if (q < t.nwin_f) {
+#pragma unroll
+        for (int j = 0; j < NH; ++j) {
+          const int f = lane + 64 * j;
+          if (f <= N / 2) accumulate_cross(X[f], X[f == 0 ? 0 : N - f], Cf[j]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NH; ++j) {
+          const int f = lane + 64 * j;
+          if (f <= N / 2) accumulate_cross(X[f], X[f == 0 ? 0 : N - f], Co[j]);
+        }
+      }
+      wave_sync();
+    }
+  }
+
+  // Y with Y[k].x = N * IDFT(Cf)[k], -Y[k].y = N * IDFT(Co)[k] (read through c())
+  __device__ const float2* inverse(const float2 (&Cf)[NH], const float2 (&Co)[NH]) {
+    store_conj_hermitian<N, NH>(bufA, Cf, Co, lane, [](int f) { return f; });
+    wave_sync();
+    return FftPlan<N>::T::run(bufA, bufB, tw, lane);
+  }
+
+  __device__ const float2* correlate(const RowTask& t, const RowTask& nt, bool has_next, int w, int hop) {
+    float2 Cf[NH], Co[NH];
+    spectra(t, nt, has_next, w, hop, Cf, Co);
+    return inverse(Cf, Co);
+  }
+
+  // twiddle exp(-2 pi i m / N), m in [0, N)
+  __device__ float2 twiddle(int m) const { return tw[m]; }
+
+  // (N * sum_s c_f[k], N * sum_s c_o[k])
+  __device__ float2 c(const float2* Y, int k, int w) const {
+    float2 v = Y[k];
+    if (PAD && k > 0) {
+      const float2 u = Y[N - w + k];
+      v.x += u.x;
+      v.y += u.y;
+    }
+    return make_float2(v.x, -v.y);
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// 20 x 25 register transform for N = 500.
+//   stage 1 (radix 20, span 1):  butterfly i < 25 reads x[i + 25 t], t < 20, writes X1[20 i + q]
+//   stage 2 (radix 25, span 20): butterfly k < 20 reads X1[k + 20 t] * W500^(t k), t < 25,
+//                                writes X[k + 20 q] (natural order, in place of what it read)
+// Stage buffers use the rotation swizzle n = 20 a + b -> 20 a + (a + b) mod 20 (bank spread for the
+// stage-1 stores, stage-2 accesses stay contiguous per row).
+
+__device__ __forceinline__ float2 tw20(int m) { return make_float2(Tw20::c[m % 20], Tw20::s[m % 20]); }
+__device__ __forceinline__ float2 tw25(int m) { return make_float2(Tw25::c[m % 25], Tw25::s[m % 25]); }
+
+// in-place natural-order DFT of length 20 (4 x 5 Cooley-Tukey, n = 5 n1 + n2, k = k1 + 4 k2)
+__device__ __forceinline__ void dft20(float2 (&x)[20]) {
+  float2 y[4][5];
+#pragma unroll
+  for (int n2 = 0; n2 < 5; ++n2) {
+    float2 v[4] = {x[n2], x[5 + n2], x[10 + n2], x[15 + n2]};
+    Dft<4>::run(v);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) y[k1][n2] = (n2 * k1 == 0) ? v[k1] : cmul(v[k1], tw20(n2 * k1));
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    float2 u[5] = {y[k1][0], y[k1][1], y[k1][2], y[k1][3], y[k1][4]};
+    Dft<5>::run(u);
+#pragma unroll
+    for (int k2 = 0; k2 < 5; ++k2) x[k1 + 4 * k2] = u[k2];
+  }
+}
+
+// in-place natural-order DFT of length 25 (5 x 5, n = 5 n1 + n2, k = k1 + 5 k2)
+__device__ __forceinline__ void dft25(float2 (&x)[25]) {
+  float2 y[5][5];
+#pragma unroll
+  for (int n2 = 0; n2 < 5; ++n2) {
+    float2 v[5] = {x[n2], x[5 + n2], x[10 + n2], x[15 + n2], x[20 + n2]};
+    Dft<5>::run(v);
+#pragma unroll
+    for (int k1 = 0; k1 < 5; ++k1) y[k1][n2] = (n2 * k1 == 0) ? v[k1] : cmul(v[k1], tw25(n2 * k1));
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 5; ++k1) {
+    float2 u[5] = {y[k1][0], y[k1][1], y[k1][2], y[k1][3], y[k1][4]};
+    Dft<5>::run(u);
+#pragma unroll
+    for (int k2 = 0; k2 < 5; ++k2) x[k1 + 5 * k2] = u[k2];
+  }
+}
+
+// Stage buffers: natural index n = 20 a + b stored at 21 a + b (row pad: conflict-free stage-1
+// stores, stage-2 column accesses at compile-time immediate offsets); buffers kBuf apart, kBuf = 20
+// mod 32 so the two sub-windows a 32-lane half touches use disjoint banks.
+__device__ __forceinline__ int pad500(int n) {
+  const int a = n / 20;
+  return n + a;
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+struct Eng500 {
+  static constexpr int N = 500;
+  static constexpr int NFFT = 500;
+  static constexpr int NJ = 8;
+  static constexpr int NH = 4;
+  static constexpr int kWaves = 7;                                              // 448-thread blocks
+  static constexpr int kSlab = 1024;                                            // floats per channel (64-lane DMA granules)
+  static constexpr int kBuf = 532;                                              // float2 per stage buffer
+  static constexpr size_t kBlockBytes = sizeof(float2) * N;                     // W500 twiddle table
+  static constexpr size_t kWaveBytes = 2 * kSlab * sizeof(float) + 3 * kBuf * sizeof(float2);  // 20960 B
+  float2* tw;
+  float* sp;   // pivot slice
+  float* sr;   // receiver slice
+  float2* B;   // 3 stage buffers
+  int lane;
+  bool pref;   // slab already holds the first slice of the next task
+  bool live_f, live_o;
+
+  __device__ Eng500(char* lds, int wave, int lane_) : lane(lane_), pref(false), live_f(false), live_o(false) {
+    tw = reinterpret_cast<float2*>(lds);
+    char* base = lds + kBlockBytes + (size_t)wave * kWaveBytes;
+    sp = reinterpret_cast<float*>(base);
+    sr = sp + kSlab;
+    B = reinterpret_cast<float2*>(base + 2 * kSlab * sizeof(float));
+  }
+  static __device__ void block_init(char* lds) {
+    float2* t = reinterpret_cast<float2*>(lds);
+    for (int m = threadIdx.x; m < N; m += blockDim.x) t[m] = kTw500[m];
+  }
+
+  // slices of a task: side f in groups of <= 3 sub-windows, then side o
+  static __device__ __forceinline__ int n_groups(int nwin) { return (nwin + 2) / 3; }
+
+  __device__ __forceinline__ void slice_of(const RowTask& t, int g, int hop, int& a, int& ns, bool& fwd) const {
+    const int gf = n_groups(t.nwin_f);
+    fwd = g < gf;
+    const int gg = fwd ? g : g - gf;
+    const int nw = fwd ? t.nwin_f : t.nwin_o;
+    ns = min(3, nw - 3 * gg);
+    a = (fwd ? t.a_f : t.a_o) + 3 * gg * hop;
+  }
+
+  // asynchronous global -> LDS copy of span samples of both channels (lane-linear destination)
+  __device__ __forceinline__ void dma(const RowTask& t, int a, int span) {
+#pragma unroll 1
+    for (int m = 0; m < (span + 63) / 64; ++m) {
+      const int n = min(64 * m + lane, span - 1);
+      __builtin_amdgcn_global_load_lds((glb_void_t*)(t.piv + a + n), (lds_void_t*)(sp + 64 * m), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_void_t*)(t.rcv + a + n), (lds_void_t*)(sr + 64 * m), 4, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void dma_slice(const RowTask& t, int g, int w, int hop) {
+    int a, ns;
+    bool fwd;
+    slice_of(t, g, hop, a, ns, fwd);
+    dma(t, a, (ns - 1) * hop + w);
+  }
+
+  // stage 1 for ns sub-windows at slab offsets s * hop (radix-20 butterflies, 2 rounds); returns the
+  // mask of sub-windows whose pivot and receiver slices both hold a non-zero sample
+  __device__ __forceinline__ uint32_t stage1(int ns, int hop, float2* out) const {
+    uint32_t live = 0;
+#pragma unroll 1
+    for (int r = 0; r < 2; ++r) {
+      const int tt = lane + 64 * r;
+      const int s = tt / 25, i = tt - 25 * (tt / 25);
+      uint32_t bp = 0, br = 0;
+      if (s < ns) {
+        const float* pp = sp + s * hop + i;
+        const float* rr = sr + s * hop + i;
+        // DFT20 over t = 5 n1 + n2 of z[i + 25 t], output q = k1 + 4 k2, streamed per n2 column
+        float2 y[4][5];
+#pragma unroll
+        for (int n2 = 0; n2 < 5; ++n2) {
+          float2 v[4];
+#pragma unroll
+          for (int n1 = 0; n1 < 4; ++n1) {
+            v[n1] = make_float2(pp[25 * (5 * n1 + n2)], rr[25 * (5 * n1 + n2)]);
+            bp |= nzbits(v[n1].x);
+            br |= nzbits(v[n1].y);
+          }
+          Dft<4>::run(v);
+#pragma unroll
+          for (int k1 = 0; k1 < 4; ++k1) y[k1][n2] = (n2 * k1 == 0) ? v[k1] : cmul(v[k1], tw20(n2 * k1));
+        }
+        float2* o = out + kBuf * s + 21 * i;
+#pragma unroll
+        for (int k1 = 0; k1 < 4; ++k1) {
+          float2 u[5] = {y[k1][0], y[k1][1], y[k1][2], y[k1][3], y[k1][4]};
+          Dft<5>::run(u);
+#pragma unroll
+          for (int k2 = 0; k2 < 5; ++k2) o[k1 + 4 * k2] = u[k2];
+        }
+      }
+      // lanes of sub-window s in this round: tt in [25 s, 25 s + 25)
+      const uint64_t mp = __ballot(bp != 0), mr = __ballot(br != 0);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int lo = max(25 * q - 64 * r, 0), hi = min(25 * q + 25 - 64 * r, 64);
+        if (lo < hi) {
+          const uint64_t rng = (hi - lo == 64 ? ~0ull : ((1ull << (hi - lo)) - 1)) << lo;
+          if ((mp & rng) && (mr & rng)) live |= 1u << q;
+        }
+      }
+    }
+    return live;
+  }
+
+  // stage 2 in place on ns buffers (radix-25 butterflies with W500 twiddles, 1 round)
+  __device__ __forceinline__ void stage2(int ns, float2* buf) const {
+    const int s = lane / 20, k = lane - 20 * (lane / 20);
+    if (s < ns) {
+      float2* b = buf + kBuf * s + k;
+      // DFT25 over t = 5 n1 + n2 of x[t] = X1[k + 20 t] * W500^(t k), output q = k1 + 5 k2,
+      // streamed one n2 column at a time to bound the live registers
+      float2 y[5][5];
+#pragma unroll
+      for (int n2 = 0; n2 < 5; ++n2) {
+        float2 v[5];
+#pragma unroll
+        for (int n1 = 0; n1 < 5; ++n1) {
+          const int t = 5 * n1 + n2;
+          v[n1] = t == 0 ? b[0] : cmul(b[21 * t], tw[t * k]);
+        }
+        Dft<5>::run(v);
+#pragma unroll
+        for (int k1 = 0; k1 < 5; ++k1) y[k1][n2] = (n2 * k1 == 0) ? v[k1] : cmul(v[k1], tw25(n2 * k1));
+      }
+#pragma unroll
+      for (int k1 = 0; k1 < 5; ++k1) {
+        float2 u[5] = {y[k1][0], y[k1][1], y[k1][2], y[k1][3], y[k1][4]};
+        Dft<5>::run(u);
+#pragma unroll
+        for (int k2 = 0; k2 < 5; ++k2) b[21 * (k1 + 5 * k2)] = u[k2];
+      }
+    }
+  }
+
+  __device__ __forceinline__ void extract(int ns, uint32_t live, float2 (&C)[NH]) const {
+#pragma unroll 1
+    for (int s = 0; s < ns; ++s) {
+      if (!((live >> s) & 1u)) continue;
+      const float2* b = B + kBuf * s;
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const int f = lane + 64 * j;
+        if (f <= N / 2) accumulate_cross(b[pad500(f)], b[pad500(f == 0 ? 0 : N - f)], C[j]);
+      }
+    }
+  }
+
+  __device__ void spectra(const RowTask& t, const RowTask& nt, bool has_next, int w, int hop, float2 (&Cf)[NH],
+                          float2 (&Co)[NH]) {
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      Cf[j] = make_float2(0.f, 0.f);
+      Co[j] = make_float2(0.f, 0.f);
+    }
+    const int ng = n_groups(t.nwin_f) + n_groups(t.nwin_o);
+    bool next_issued = false;
+    live_f = live_o = false;
+    if (!pref && ng > 0) dma_slice(t, 0, w, hop);
+    pref = false;
+    for (int g = 0; g < ng; ++g) {
+      int a, ns;
+      bool fwd;
+      slice_of(t, g, hop, a, ns, fwd);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wave_sync();
+      const uint32_t lm = stage1(ns, hop, B);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wave_sync();
+      // the slab is free: start the next slice's copy under stage 2 / extraction / inverse FFT
+      if (g + 1 < ng) {
+        dma_slice(t, g + 1, w, hop);
+      } else if (has_next && (n_groups(nt.nwin_f) + n_groups(nt.nwin_o)) > 0) {
+        dma_slice(nt, 0, w, hop);
+        next_issued = true;
+      }
+      stage2(ns, B);
+      wave_sync();
+      if (fwd) {
+        extract(ns, lm, Cf);
+        live_f |= lm != 0;
+      } else {
+        extract(ns, lm, Co);
+        live_o |= lm != 0;
+      }
+      wave_sync();
+    }
+    if (!next_issued && has_next && (n_groups(nt.nwin_f) + n_groups(nt.nwin_o)) > 0) {
+      dma_slice(nt, 0, w, hop);
+      next_issued = true;
+    }
+    pref = next_issued;
+  }
+
+  // inverse transform of W = Cf + i Co through conj(FFT(conj(W))): natural input in B[0, 500),
+  // stage 1 -> buffer 1 (padded), stage 2 in place
+  __device__ const float2* inverse(const float2 (&Cf)[NH], const float2 (&Co)[NH]) {
+    store_conj_hermitian<N, NH>(B, Cf, Co, lane, [](int f) { return f; });
+    wave_sync();
+    if (lane < 25) {
+      float2 x[20];
+#pragma unroll
+      for (int t = 0; t < 20; ++t) x[t] = B[lane + 25 * t];
+      dft20(x);
+      float2* o = B + kBuf + 21 * lane;
+#pragma unroll
+      for (int q = 0; q < 20; ++q) o[q] = x[q];
+    }
+    wave_sync();
+    stage2(1, B + kBuf);
+    wave_sync();
+    return B + kBuf;
+  }
+
+  __device__ const float2* correlate(const RowTask& t, const RowTask& nt, bool has_next, int w, int hop) {
+    float2 Cf[NH], Co[NH];
+    spectra(t, nt, has_next, w, hop, Cf, Co);
+    return inverse(Cf, Co);
+  }
+
+  __device__ float2 twiddle(int m) const { return tw[m]; }
+
+  __device__ float2 c(const float2* Y, int k, int) const {
+    const float2 v = Y[pad500(k)];
+    return make_float2(v.x, -v.y);
+  }
+};
+
+}  // namespace dvh

@@ -70,3 +70,54 @@ def test_edge_cases(device, case):
     assert gio.gather_rel_err(vsg.XCF_out, g[case + "_xcf"]) < TOL
     assert np.array_equal(vsg.x_axis, g[case + "_gx"])
     assert np.array_equal(vsg.t_axis, g[case + "_gt"])
+
+
+@pytest.mark.parametrize("fixture", ["vsg_w500", "vsg_w499"])
+@pytest.mark.parametrize("kw", [
+    dict(include_other_side=True, norm=False),
+    dict(include_other_side=True),
+    dict(include_other_side=False),
+    dict(include_other_side=True, norm=False, norm_amp=False),
+    dict(include_other_side=False, norm=False),
+])
+@pytest.mark.parametrize("special", [False, True])
+def test_stack_modes(device, fixture, kw, special):
+    """Fused correlate-and-stack for every flag combination, two classes, against the oracle.
+    With ``special`` passes get half their channels zeroed (one side of the gather is 0/0 and must
+    drop out of the two-sided average), all channels zeroed, or a NaN sample, which must propagate
+    exactly as sum(images)/len(images) does in the reference (imaging_classes.py:127)."""
+    from das_diff_veh_amd import engine
+    from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+    from das_diff_veh_amd.plan import VsgParams
+    from oracle import vsg as ovsg
+    g = gio.load(fixture)
+    n = gio.n_pass(g)
+    arrs = [gio.pass_arrays(g, i) for i in range(n)]
+    if special:
+        for i, kind in zip(range(n), ["low", "high", "zero", "nan"]):
+            d = arrs[i]["data"].copy()
+            half = d.shape[0] // 2
+            if kind == "low":
+                d[:half] = 0
+            elif kind == "high":
+                d[half:] = 0
+            elif kind == "zero":
+                d[:] = 0
+            else:
+                d[5, 1000] = np.nan
+            arrs[i]["data"] = d
+    wins = [SurfaceWaveWindow(**a) for a in arrs]
+    slots = np.array([i % 2 for i in range(n)])
+    prm = VsgParams(**kw, **KW)
+    got, _ = engine.stacked(wins, prm, slots=slots, n_slot=2, device=device, chunk=2)
+    got = got.double().cpu().numpy()
+    for s in range(2):
+        refs = []
+        for i in np.where(slots == s)[0]:
+            o = gio.oracle_window(g, i)
+            o["data"] = arrs[i]["data"].astype(np.float64)
+            with np.errstate(all="ignore"):
+                refs.append(ovsg.virtual_shot_gather(o, **kw, **KW)[0])
+        with np.errstate(all="ignore"):
+            ref = ovsg.stack(refs)
+        assert gio.gather_rel_err(got[s], ref) < TOL, (s, kw)
