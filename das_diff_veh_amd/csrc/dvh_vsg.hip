@@ -40,6 +40,7 @@ constexpr int kBlock = 256;  // sumsq kernel
 // waves per SIMD the kernels are compiled for: one 7-wave Eng500 block (145 KB LDS) per CU;
 // the Stockham engines are register-limited to 3
 template <class E> struct Occ { static constexpr int v = 3; };
+template <> struct Occ<EngF500> { static constexpr int v = 4; };
 template <> struct Occ<Eng500> { static constexpr int v = 2; };
 #ifndef DVH_STACKF_OCC
 #define DVH_STACKF_OCC 0
@@ -356,8 +357,8 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
       float s2f = 0.f, s2o = 0.f;
 #pragma unroll
       for (int m = 0; m < NH; ++m) {
-        const int f = lane + 64 * m;
-        if (f <= h) {
+        const int f = E::bin(lane, m);
+        if (f >= 0) {
           bad |= isnan(Cf[m].x) || isnan(Cf[m].y) || isnan(Co[m].x) || isnan(Co[m].y);
           nzo |= (Co[m].x != 0.f) || (Co[m].y != 0.f);
           // Parseval over all N bins from the half spectrum: interior bins count twice
@@ -401,8 +402,8 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
         const int so_shift = oth_shared ? h - 1 : h;
 #pragma unroll
         for (int m = 0; m < NH; ++m) {
-          const int f = lane + 64 * m;
-          if (f <= h) {
+          const int f = E::bin(lane, m);
+          if (f >= 0) {
             float2 x = fwd_shared ? make_float2(Cf[m].x, -Cf[m].y) : Cf[m];
             x = cmul(x, eng.twiddle((sf_shift * f) % N));
             Gh[m].x += cf * x.x;
@@ -499,8 +500,10 @@ static bool get_kernels(int w, VsgKernels* k, int* n_out) {
   *n_out = n;
   switch (n) {
     case 250: *k = vsg_kernels<EngStockham<250, false>, true>(); return true;
-    case 500:
-      *k = DVH_VSG500 ? vsg_kernels<Eng500, true>() : vsg_kernels<EngStockham<500, false>, true>();
+    case 500:  // 0: fused-stage Stockham (default), 1: 20 x 25 register engine, 2: plain Stockham
+      *k = DVH_VSG500 == 1   ? vsg_kernels<Eng500, true>()
+           : DVH_VSG500 == 2 ? vsg_kernels<EngStockham<500, false>, true>()
+                             : vsg_kernels<EngF500, true>();
       return true;
     case 1000: *k = vsg_kernels<EngStockham<1000, false>, true>(); return true;
     case 512: *k = vsg_kernels<EngStockham<512, true>, false>(); return true;

@@ -14,6 +14,9 @@
 #ifndef DVH_STAGE_UNROLL
 #define DVH_STAGE_UNROLL 0
 #endif
+#ifndef DVH_TW_RECUR
+#define DVH_TW_RECUR 1
+#endif
 
 namespace dvh {
 
@@ -106,8 +109,19 @@ __device__ __forceinline__ void stockham_stage(const float2* __restrict__ in, fl
 #pragma unroll
       for (int t = 0; t < R; ++t) a[t] = in[i + t * NB];
       if (Ls > 1) {
+#if DVH_TW_RECUR
+        // one table read per butterfly, powers by recurrence (LDS reads are the scarcer resource)
+        const float2 w1 = tw[k * TWS];
+        float2 wt = w1;
+#pragma unroll
+        for (int t = 1; t < R; ++t) {
+          a[t] = cmul(a[t], wt);
+          if (t + 1 < R) wt = cmul(wt, w1);
+        }
+#else
 #pragma unroll
         for (int t = 1; t < R; ++t) a[t] = cmul(a[t], tw[t * k * TWS]);
+#endif
       }
       Dft<R>::run(a);
       const int base = (i - k) * R + k;

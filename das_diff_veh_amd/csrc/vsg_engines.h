@@ -99,17 +99,19 @@ __device__ __forceinline__ void accumulate_cross(float2 Az, float2 Bc, float2& C
   C.y += 0.25f * ((Az.x * Az.x + Az.y * Az.y) - (bx * bx + by * by));
 }
 
-// conj(W) for W = Cf + i Co over all N bins from the half spectra (bins f <= N/2): the input of the
-// inverse transform conj(FFT(conj(W))).  W[N - f] = conj(Cf[f]) + i conj(Co[f]).
-template <int N, int NH, class Idx>
-__device__ __forceinline__ void store_conj_hermitian(float2* buf, const float2 (&Cf)[NH], const float2 (&Co)[NH],
-                                                     int lane, Idx idx) {
+// conj(W) for W = Cf + i Co over all N bins from the half spectra held in the engine's slots
+// (slot j of a lane is bin E::bin(lane, j) <= N/2, or -1): the input of the inverse transform
+// conj(FFT(conj(W))).  W[N - f] = conj(Cf[f]) + i conj(Co[f]).
+template <class E>
+__device__ __forceinline__ void store_conj_hermitian(float2* buf, const float2 (&Cf)[E::NH], const float2 (&Co)[E::NH],
+                                                     int lane) {
+  constexpr int N = E::NFFT;
 #pragma unroll
-  for (int j = 0; j < NH; ++j) {
-    const int f = lane + 64 * j;
-    if (f <= N / 2) {
-      buf[idx(f)] = make_float2(Cf[j].x - Co[j].y, -(Cf[j].y + Co[j].x));
-      if (f > 0 && f < N / 2) buf[idx(N - f)] = make_float2(Cf[j].x + Co[j].y, Cf[j].y - Co[j].x);
+  for (int j = 0; j < E::NH; ++j) {
+    const int f = E::bin(lane, j);
+    if (f >= 0) {
+      buf[E::slot(f)] = make_float2(Cf[j].x - Co[j].y, -(Cf[j].y + Co[j].x));
+      if (f > 0 && f < N / 2) buf[E::slot(N - f)] = make_float2(Cf[j].x + Co[j].y, Cf[j].y - Co[j].x);
     }
   }
 }
@@ -194,8 +196,15 @@ struct EngStockham {
   }
 
   // Y with Y[k].x = N * IDFT(Cf)[k], -Y[k].y = N * IDFT(Co)[k] (read through c())
+  // half-spectrum slot j of a lane holds bin f = lane + 64 j (f <= N/2)
+  static __device__ __forceinline__ int bin(int lane, int j) {
+    const int f = lane + 64 * j;
+    return f <= N / 2 ? f : -1;
+  }
+  static __device__ __forceinline__ int slot(int n) { return n; }
+
   __device__ const float2* inverse(const float2 (&Cf)[NH], const float2 (&Co)[NH]) {
-    store_conj_hermitian<N, NH>(bufA, Cf, Co, lane, [](int f) { return f; });
+    store_conj_hermitian<EngStockham>(bufA, Cf, Co, lane);
     wave_sync();
     return FftPlan<N>::T::run(bufA, bufB, tw, lane);
   }
@@ -480,8 +489,14 @@ struct Eng500 {
 
   // inverse transform of W = Cf + i Co through conj(FFT(conj(W))): natural input in B[0, 500),
   // stage 1 -> buffer 1 (padded), stage 2 in place
+  static __device__ __forceinline__ int bin(int lane, int j) {
+    const int f = lane + 64 * j;
+    return f <= N / 2 ? f : -1;
+  }
+  static __device__ __forceinline__ int slot(int n) { return n; }
+
   __device__ const float2* inverse(const float2 (&Cf)[NH], const float2 (&Co)[NH]) {
-    store_conj_hermitian<N, NH>(B, Cf, Co, lane, [](int f) { return f; });
+    store_conj_hermitian<Eng500>(B, Cf, Co, lane);
     wave_sync();
     if (lane < 25) {
       float2 x[20];
@@ -508,6 +523,166 @@ struct Eng500 {
 
   __device__ float2 c(const float2* Y, int k, int) const {
     const float2 v = Y[pad500(k)];
+    return make_float2(v.x, -v.y);
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// EngF500: N = w = 500 Stockham (4 x 5 x 5 x 5) with the first and last stages fused into registers.
+//   stage 1 (radix 4, span 1) reads its inputs straight from the prefetched sub-window samples
+//     (lane i < 125 of round r holds samples i + 125 t) -- no LDS store of the raw window;
+//   stages 2-3 go through LDS (one twiddle read per butterfly, powers by recurrence);
+//   stage 4 (radix 5, span 100) runs butterflies k and 100 - k in the same lane (l <= 50), so the
+//     lane holds X[k + 100 q] and its Hermitian partners X[N - f] and forms the cross spectra of its
+//     five bins in registers -- no LDS write of the spectrum and no partner reads.
+// Half-spectrum slots per lane l: j < 3 -> f = l + 100 j (l <= 50); j = 3, 4 -> f = 100 - l + 100 (j - 3)
+// (1 <= l <= 49): each of the 251 bins f <= 250 exactly once.
+struct EngF500 {
+  static constexpr int N = 500;
+  static constexpr int NFFT = 500;
+  static constexpr int NJ = 8;
+  static constexpr int NH = 5;
+  static constexpr int kWaves = 4;
+  static constexpr size_t kBlockBytes = sizeof(float2) * N;     // twiddle table
+  static constexpr size_t kWaveBytes = sizeof(float2) * 2 * N;  // ping-pong buffers
+  float2* tw;
+  float2* bufA;
+  float2* bufB;
+  int lane;
+  bool live_f, live_o;
+
+  __device__ EngF500(char* lds, int wave, int lane_) : lane(lane_), live_f(false), live_o(false) {
+    tw = reinterpret_cast<float2*>(lds);
+    bufA = reinterpret_cast<float2*>(lds + kBlockBytes + (size_t)wave * kWaveBytes);
+    bufB = bufA + N;
+  }
+  static __device__ void block_init(char* lds) { init_twiddles<N>(reinterpret_cast<float2*>(lds)); }
+
+  static __device__ __forceinline__ int bin(int l, int j) {
+    if (j < 3) return l <= 50 ? l + 100 * j : -1;
+    return (l >= 1 && l <= 49) ? 100 - l + 100 * (j - 3) : -1;
+  }
+  static __device__ __forceinline__ int slot(int n) { return n; }
+
+  // stage-1 operands of a sub-window starting at a: z[4 r + t] = (pivot, receiver)[i + 125 t], i = lane + 64 r
+  __device__ __forceinline__ void load(const RowTask& t, int a, float2 (&z)[8]) const {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = lane + 64 * r;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int n = a + i + 125 * u;
+        z[4 * r + u] = (i < 125) ? make_float2(t.piv[n], t.rcv[n]) : make_float2(0.f, 0.f);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void stage1(const float2 (&z)[8]) const {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = lane + 64 * r;
+      if (r == 0 || i < 125) {
+        float2 a[4] = {z[4 * r], z[4 * r + 1], z[4 * r + 2], z[4 * r + 3]};
+        Dft<4>::run(a);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bufB[4 * i + q] = a[q];
+      }
+    }
+  }
+
+  // stages 2-4 of the transform whose stage-1 output is in bufB; cross spectra into C
+  __device__ __forceinline__ void finish(float2 (&C)[NH]) const {
+    wave_sync();
+    stockham_stage<N, 4, 5>(bufB, bufA, tw, lane);
+    wave_sync();
+    stockham_stage<N, 20, 5>(bufA, bufB, tw, lane);
+    wave_sync();
+    if (lane <= 50) {
+      float2 XA[5], XB[5];
+      last_bfly_from(bufB, lane, XA);
+      const bool pair = lane >= 1 && lane <= 49;
+      if (pair) last_bfly_from(bufB, 100 - lane, XB);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        // partner X[N - f] of f = l + 100 j is X[(100 - l) + 100 (4 - j)]
+        const float2 p0 = XA[(5 - j) % 5], p50 = XA[4 - j], pb = XB[4 - j];
+        float2 pa;  // value selects (a select of array elements would become a scratch pointer)
+        pa.x = lane == 0 ? p0.x : (lane == 50 ? p50.x : pb.x);
+        pa.y = lane == 0 ? p0.y : (lane == 50 ? p50.y : pb.y);
+        accumulate_cross(XA[j], pa, C[j]);
+      }
+      if (pair) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) accumulate_cross(XB[q], XA[4 - q], C[3 + q]);
+      }
+    }
+    wave_sync();
+  }
+
+  // radix-5 butterfly k of the last stage (span 100): X[k + 100 q], q < 5
+  __device__ __forceinline__ void last_bfly_from(const float2* src, int k, float2 (&x)[5]) const {
+#pragma unroll
+    for (int t = 0; t < 5; ++t) x[t] = src[k + 100 * t];
+    const float2 w1 = tw[k];
+    float2 wt = w1;
+#pragma unroll
+    for (int t = 1; t < 5; ++t) {
+      x[t] = cmul(x[t], wt);
+      if (t < 4) wt = cmul(wt, w1);
+    }
+    Dft<5>::run(x);
+  }
+
+  __device__ void spectra(const RowTask& t, const RowTask&, bool, int, int hop, float2 (&Cf)[NH], float2 (&Co)[NH]) {
+    const int nq = t.nwin_f + t.nwin_o;
+    float2 z[8];
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      Cf[j] = make_float2(0.f, 0.f);
+      Co[j] = make_float2(0.f, 0.f);
+    }
+    live_f = live_o = false;
+    if (nq > 0) load(t, t.nwin_f > 0 ? t.a_f : t.a_o, z);
+    for (int q = 0; q < nq; ++q) {
+      uint32_t bp = 0, br = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bp |= nzbits(z[j].x);
+        br |= nzbits(z[j].y);
+      }
+      const bool live = (__ballot(bp != 0) != 0) && (__ballot(br != 0) != 0);
+      if (live) stage1(z);
+      if (q + 1 < nq) {
+        const int qn = q + 1;
+        load(t, qn < t.nwin_f ? t.a_f + qn * hop : t.a_o + (qn - t.nwin_f) * hop, z);
+      }
+      if (!live) continue;  // exactly zero in the reference
+      if (q < t.nwin_f) {
+        live_f = true;
+        finish(Cf);
+      } else {
+        live_o = true;
+        finish(Co);
+      }
+    }
+  }
+
+  __device__ const float2* inverse(const float2 (&Cf)[NH], const float2 (&Co)[NH]) {
+    store_conj_hermitian<EngF500>(bufA, Cf, Co, lane);
+    wave_sync();
+    return FftPlan<N>::T::run(bufA, bufB, tw, lane);
+  }
+
+  __device__ const float2* correlate(const RowTask& t, const RowTask& nt, bool has_next, int w, int hop) {
+    float2 Cf[NH], Co[NH];
+    spectra(t, nt, has_next, w, hop, Cf, Co);
+    return inverse(Cf, Co);
+  }
+
+  __device__ float2 twiddle(int m) const { return tw[m]; }
+
+  __device__ float2 c(const float2* Y, int k, int) const {
+    const float2 v = Y[k];
     return make_float2(v.x, -v.y);
   }
 };
