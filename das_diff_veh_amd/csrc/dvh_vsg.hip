@@ -70,6 +70,16 @@ __device__ __forceinline__ E make_engine(char* lds) {
   return E(lds, threadIdx.x >> 6, threadIdx.x & 63);
 }
 
+// The reference divides every window by ||data||_F first (preprocessing_window,
+// apis/virtual_shot_gather.py:125): a window holding a NaN / inf, or all zero (0 / 0), turns the
+// whole gather into NaN.  With win_sumsq = ||data||_F^2 given, such a pass gets NaN scales, which
+// the gather / stack kernels carry into every computed row exactly as that division does.
+__device__ __forceinline__ bool window_invalid(const double* __restrict__ sumsq, int p) {
+  if (!sumsq) return false;
+  const double s = sumsq[p];
+  return !(s > 0.0) || !isfinite(s);
+}
+
 // Per-pass scale of each side: 1 / max(pivot autocorrelation row) after the optional row norm
 // (post_processing_XCF with norm_amp=True); 1 / ||window||_F^2 when neither norm is requested.
 template <class E>
@@ -85,9 +95,9 @@ __global__ __launch_bounds__(64 * E::kWaves, Occ<E>::v) void vsg_scales_kernel(V
   constexpr int NJ = E::NJ;
   const int stride = gridDim.x * E::kWaves;
   for (int p = blockIdx.x * E::kWaves + wave; p < A.n_pass; p += stride) {
-    if (!norm_amp) {
+    if (!norm_amp || window_invalid(sumsq, p)) {
       if (lane == 0) {
-        const float s = norm ? 1.0f : (float)(1.0 / sumsq[p]);
+        const float s = window_invalid(sumsq, p) ? NAN : (norm ? 1.0f : (float)(1.0 / sumsq[p]));
         scales[2 * p] = s;
         scales[2 * p + 1] = s;
       }

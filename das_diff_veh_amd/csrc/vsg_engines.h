@@ -592,6 +592,13 @@ struct EngF500 {
 
   // stages 2-4 of the transform whose stage-1 output is in bufB; cross spectra into C
   __device__ __forceinline__ void finish(float2 (&C)[NH]) const {
+    finish_with([&](int j, float2 a, float2 b) { accumulate_cross(a, b, C[j]); });
+  }
+
+  // stages 2-4 of the transform whose stage-1 output is in bufB; for every half-spectrum slot j of
+  // the lane (compile-time j, valid slots only), acc(j, Z[f], Z[N - f]) with f = bin(lane, j)
+  template <class F>
+  __device__ __forceinline__ void finish_with(F&& acc) const {
     wave_sync();
     stockham_stage<N, 4, 5>(bufB, bufA, tw, lane);
     wave_sync();
@@ -609,11 +616,11 @@ struct EngF500 {
         float2 pa;  // value selects (a select of array elements would become a scratch pointer)
         pa.x = lane == 0 ? p0.x : (lane == 50 ? p50.x : pb.x);
         pa.y = lane == 0 ? p0.y : (lane == 50 ? p50.y : pb.y);
-        accumulate_cross(XA[j], pa, C[j]);
+        acc(j, XA[j], pa);
       }
       if (pair) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) accumulate_cross(XB[q], XA[4 - q], C[3 + q]);
+        for (int q = 0; q < 2; ++q) acc(3 + q, XB[q], XA[4 - q]);
       }
     }
     wave_sync();

@@ -6,7 +6,7 @@ stream-ordered on the current torch stream and never synchronise.
 
     scales = vsg_scales(windows, plan)                 # per-pass amplitude normalisation, [n, 2]
     g      = vsg_gathers(windows, plan, scales)        # per-pass gathers, [n, R, w]
-    s      = vsg_stack(windows, plan, slots, n_slot)   # mean gather per class slot, [n_slot, R, w]
+    s      = vsg_stack(windows, plan, schedule)        # mean gather per class slot, [n_slot, R, w]
 """
 from __future__ import annotations
 
@@ -35,12 +35,14 @@ def window_sumsq(windows: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def vsg_scales(windows: torch.Tensor, plan: VsgPlan, out: torch.Tensor | None = None) -> torch.Tensor:
+def vsg_scales(windows: torch.Tensor, plan: VsgPlan, out: torch.Tensor | None = None,
+               win_sumsq: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-pass scales [n, 2].  ``win_sumsq`` (= window_sumsq(windows), a per-window property that
+    callers imaging the same windows repeatedly compute once) also marks windows that are not
+    finite or all zero, whose gathers are NaN in the reference (data / ||data||_F)."""
     _check_windows(windows, plan)
     pass_tab, seg_tab = plan.device_tables(windows.device)
-    sumsq = None
-    if not plan.prm.norm and not plan.prm.norm_amp:
-        sumsq = window_sumsq(windows)
+    sumsq = window_sumsq(windows) if win_sumsq is None else win_sumsq
     if out is None:
         out = torch.empty((plan.n_pass, 2), dtype=torch.float32, device=windows.device)
     _lib.call("dvh_vsg_scales", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
@@ -103,17 +105,19 @@ class StackSchedule:
 
 
 def vsg_stack(windows: torch.Tensor, plan: VsgPlan, schedule: StackSchedule, scales: torch.Tensor | None = None,
-              out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
-    """Class-mean gathers [n_slot, R, w]; with accumulate=True adds into ``out``."""
+              out: torch.Tensor | None = None, accumulate: bool = False,
+              win_sumsq: torch.Tensor | None = None) -> torch.Tensor:
+    """Class-mean gathers [n_slot, R, w]; with accumulate=True adds into ``out``.  ``scales`` come
+    from vsg_scales (formed here with ``win_sumsq`` when not given)."""
     _check_windows(windows, plan)
-    if scales is None:
-        scales = vsg_scales(windows, plan)
     pass_tab, seg_tab = plan.device_tables(windows.device)
     order, chunk_tab, weights = schedule.device_tables(windows.device)
     if out is None:
         out = torch.zeros((schedule.n_slot, plan.R, plan.w), dtype=torch.float32, device=windows.device)
     elif not accumulate:
         out.zero_()
+    if scales is None:
+        scales = vsg_scales(windows, plan, win_sumsq=win_sumsq)
     _lib.call("dvh_vsg_stack", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
               _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop, plan.flags, _lib.ptr(scales),
               _lib.ptr(order), _lib.ptr(chunk_tab), int(chunk_tab.shape[0]), _lib.ptr(weights), _lib.ptr(out),

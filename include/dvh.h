@@ -45,7 +45,9 @@ int dvh_window_sumsq(const float* win, int64_t pass_stride, int64_t ch_stride, i
 
 /* Per-pass, per-side amplitude normalisation: scales[p][side] = 1 / amax(pivot row)
  * (post_processing_XCF, apis/virtual_shot_gather.py:137-138), or 1 / ||window||_F^2 when
- * neither norm nor norm_amp is set (win_sumsq from dvh_window_sumsq). */
+ * neither norm nor norm_amp is set (win_sumsq from dvh_window_sumsq; required then, optional
+ * otherwise).  When win_sumsq is given, a pass whose window is not finite or all zero gets NaN
+ * scales: the reference's data / ||data||_F (:125) makes that whole gather NaN. */
 int dvh_vsg_scales(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, const int32_t* pass_tab,
                    const int32_t* seg_tab, int32_t R, int32_t w, int32_t hop, int32_t flags, const double* win_sumsq,
                    float* scales, void* stream);

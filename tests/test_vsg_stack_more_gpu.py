@@ -1,0 +1,92 @@
+"""More GPU parity of the fused correlate-and-stack path: passes whose pivot sits at different gather
+rows within one launch (odd row count), and windows the reference turns into NaN gathers
+(data / ||data||_F with a NaN, apis/virtual_shot_gather.py:125)."""
+import numpy as np
+import pytest
+
+from tests import golden_io as gio
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+KW = dict(pivot=700, start_x=500, end_x=900, wlen=2)
+
+
+def _fixture_batch(device, name="vsg_w500", **kw):
+    import torch
+
+    from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+    from das_diff_veh_amd.plan import VsgParams, VsgPlan, pass_geometry
+    g = gio.load(name)
+    wins = [SurfaceWaveWindow(**gio.pass_arrays(g, i)) for i in range(gio.n_pass(g))]
+    prm = VsgParams(**{**KW, **kw})
+    geoms = [pass_geometry(w.x_axis, w.t_axis, w.veh_state_x, w.veh_state_t, prm) for w in wins]
+    data = torch.as_tensor(np.stack([w.data for w in wins]), device=device)
+    return g, wins, prm, VsgPlan(geoms, prm, data.shape[1], data.shape[2]), data
+
+
+def _mixed_batch(device, n_each=12, seed=5):
+    """Passes generated at two fiber offsets: the pivot is gather row 24 for one half, 25 for the
+    other (R = 49 for both), so shared and trajectory rows differ between passes of one launch."""
+    import torch
+
+    from das_diff_veh_amd.synth import synth_batch_device
+    out = []
+    for off in (0.0, 4.0):
+        w, x, t, trk, _ = synth_batch_device(n_each, pivot=700.0, seed=seed + int(off), device=device,
+                                             x_first=700 - 30 * 8.16 + off)
+        out.append((w, x, t, trk))
+    wins = torch.cat([o[0] for o in out])
+    xs = [o[1] for o in out for _ in range(n_each)]
+    ts = [o[2] for o in out for _ in range(n_each)]
+    trk = [tr for o in out for tr in o[3]]
+    return wins, xs, ts, trk
+
+
+@pytest.mark.parametrize("kw", [dict(include_other_side=True, norm=False), dict(include_other_side=True),
+                                dict(include_other_side=False, norm=False)])
+def test_stack_mixed_pivot_rows(device, kw):
+    from das_diff_veh_amd import vsg
+    from das_diff_veh_amd.plan import VsgParams, VsgPlan, pass_geometry
+    from oracle import vsg as ovsg
+    wins, xs, ts, trk = _mixed_batch(device)
+    prm = VsgParams(**{**KW, **kw})
+    geoms = [pass_geometry(x, t, vx, vt, prm) for x, t, (vx, vt) in zip(xs, ts, trk)]
+    assert {g.pivot_idx - g.start_idx for g in geoms} == {24, 25} and {g.end_idx - g.start_idx for g in geoms} == {49}
+    plan = VsgPlan(geoms, prm, wins.shape[1], wins.shape[2])
+    slots = np.arange(len(geoms)) % 3
+    sched = vsg.StackSchedule(slots, 3, chunk=4)
+    got = vsg.vsg_stack(wins, plan, sched).double().cpu().numpy()
+    host = wins.double().cpu().numpy()
+    for s in range(3):
+        refs = []
+        for i in np.flatnonzero(slots == s):
+            o = dict(data=host[i], x_axis=xs[i], t_axis=ts[i], veh_state_x=trk[i][0], veh_state_t=trk[i][1])
+            refs.append(ovsg.virtual_shot_gather(o, **kw, **KW)[0])
+        assert gio.gather_rel_err(got[s], ovsg.stack(refs)) < TOL, (s, kw)
+
+
+def test_stack_invalid_windows(device):
+    """A NaN anywhere in a window makes that pass's whole gather NaN (the reference divides by
+    ||data||_F, apis/virtual_shot_gather.py:125); a zeroed channel drops out exactly."""
+    from das_diff_veh_amd import vsg
+    from das_diff_veh_amd.plan import VsgPlan
+    from oracle import vsg as ovsg
+    g, wins, prm, plan, data = _fixture_batch(device, include_other_side=True, norm=False)
+    geo = plan.geoms[0]
+    a, L = geo.seg[0, 0]
+    data = data.clone()
+    data[0, geo.start_idx + 2, a + 10] = float("nan")
+    data[1, geo.start_idx + 4] = 0.0
+    host = data.double().cpu().numpy()
+    refs = []
+    for i in range(plan.n_pass):
+        p1 = VsgPlan([plan.geoms[i]], prm, plan.n_ch, plan.n_t)
+        got = vsg.vsg_stack(data[i:i + 1], p1, vsg.StackSchedule(np.zeros(1, np.int64), 1, chunk=1))
+        o = gio.oracle_window(g, i)
+        o["data"] = host[i]
+        with np.errstate(all="ignore"):
+            refs.append(ovsg.virtual_shot_gather(o, include_other_side=True, norm=False, **KW)[0])
+        assert gio.gather_rel_err(got.double().cpu().numpy()[0], refs[i]) < TOL, i
+    got = vsg.vsg_stack(data, plan, vsg.StackSchedule(np.zeros(plan.n_pass, np.int64), 1, chunk=2))
+    with np.errstate(all="ignore"):
+        assert gio.gather_rel_err(got.double().cpu().numpy()[0], ovsg.stack(refs)) < TOL
