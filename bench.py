@@ -17,6 +17,7 @@ Prints ONE JSON line (rank 0).  `value` = vehicle-pass windows per second over a
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import platform
@@ -112,25 +113,36 @@ def step(sets, world, ev=None):
         fv_from_fk(fk_grid(s.stack[:, a:b, :], s.disp), s.disp, out=s.fv)
 
 
-def cpu_baseline(sets, budget_s=20.0):
-    """Reference-structured CPU path (oracle/ref_loop.py) on a bounded sample of the same windows,
-    single core, extrapolated to one full step (all windows + every class image)."""
+def cpu_baseline(sets, budget_s=20.0, workers=None):
+    """Reference-structured CPU path (oracle/ref_loop.py) on a bounded sample of the same windows.
+
+    1 core: the bench windows themselves (host copies) for about budget_s / 2, plus one f-v image
+    per set.  All cores: `workers` single-threaded processes (spawned, no GPU state; the box's CPU
+    share is 16) each looping over a saved sample of the windows for budget_s / 2; the value is the
+    aggregate windows/s, extrapolated with the 1-core image cost to one full step."""
+    import multiprocessing as mp
+    import tempfile
+
     from oracle import ref_loop
     torch.set_num_threads(1)
+    workers = workers or max(1, min(16, os.cpu_count() or 1))
     n_win, t_win, t_img, n_img = 0, 0.0, 0.0, 0
     t_start = time.time()
-    per_set = max(4, int(budget_s / 0.05 / max(len(sets), 1)))
+    one_budget = budget_s / 2
+    per_set = max(4, int(one_budget / 0.01 / max(len(sets), 1)))
+    samples = []
     for s in sets:
         x_axis, t_axis, trk = s.host
         k = min(per_set, s.n)
         host = s.windows[:k].to("cpu", torch.float64).numpy()
+        samples.append((host[:16].astype(np.float32), x_axis, t_axis, trk[:16], s.prm))
         t0 = time.time()
         acc = None
         for i in range(k):
             g, gx, gt = ref_loop.gather(host[i], x_axis, t_axis, trk[i][0], trk[i][1], s.prm.pivot, s.prm.start_x,
                                         s.prm.end_x)
             acc = g if acc is None else acc + g
-            if time.time() - t_start > budget_s:
+            if time.time() - t_start > one_budget:
                 k = i + 1
                 break
         t_win += time.time() - t0
@@ -143,11 +155,52 @@ def cpu_baseline(sets, budget_s=20.0):
     per_image = t_img / n_img
     total_windows = sum(s.n for s in sets)
     total_images = sum(s.stack.shape[0] for s in sets)
-    step_s = per_window * total_windows + per_image * total_images
-    return dict(value=total_windows / step_s, unit="vehicle-pass windows/s", cores=1, kind="port",
-                sample=f"{n_win} windows (VSG two-sided + stack) and {n_img} f-v images timed on 1 core "
-                       f"({per_window * 1e3:.1f} ms/window, {per_image * 1e3:.1f} ms/image), extrapolated to one step "
-                       f"of {total_windows} windows + {total_images} images; cpu={platform.processor() or platform.machine()}")
+    rate1 = total_windows / (per_window * total_windows + per_image * total_images)
+    # all cores: single-threaded worker processes (plain python, no torch / GPU state) over a saved
+    # sample of the first set's windows, all running at once
+    import subprocess
+    host, x_axis, t_axis, trk, prm = samples[0]
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "sample.npz")
+        np.savez(path, wins=host, x_axis=x_axis, t_axis=t_axis, vx=np.stack([v for v, _ in trk]),
+                 vt=np.stack([t for _, t in trk]), pivot=prm.pivot, start_x=prm.start_x, end_x=prm.end_x)
+        procs = [subprocess.Popen([sys.executable, "-m", "oracle.ref_loop", path, str(w), str(budget_s / 2)],
+                                  cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+                 for w in range(workers)]
+        res = []
+        for pr in procs:
+            try:
+                out, _ = pr.communicate(timeout=budget_s * 4 + 60)
+                done, secs = out.split()
+                res.append((int(done), float(secs)))
+            except Exception:  # a worker that failed or hung does not count
+                pr.kill()
+    if not res:
+        raise RuntimeError("no CPU-baseline worker finished")
+    workers = len(res)
+    agg_window_rate = sum(n / t for n, t in res)
+    step_s = total_windows / agg_window_rate + per_image * total_images / workers
+    return dict(value=total_windows / step_s, unit="vehicle-pass windows/s", cores=workers, kind="port",
+                sample=f"all cores: {workers} single-threaded processes x {budget_s / 2:.0f} s, {sum(n for n, _ in res)} "
+                       f"windows (VSG two-sided), f-v images at the 1-core cost / {workers}; 1 core: {n_win} windows "
+                       f"({per_window * 1e3:.1f} ms/window), {n_img} f-v images ({per_image * 1e3:.1f} ms/image) -> "
+                       f"{rate1:.1f} windows/s; cpu={platform.processor() or platform.machine()}",
+                value_1core=rate1)
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/<round>_pmc_summary.json, written by tools/pmc.sh: FETCH_SIZE / WRITE_SIZE with the
+    access-width calibration measured by tools/calib/fetch_calib).  (None, None) if absent."""
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in d and "traffic_bytes" in d[kernel]:
+            return float(d[kernel]["traffic_bytes"]), os.path.basename(f)
+    return None, None
 
 
 def main():
@@ -201,6 +254,7 @@ def main():
     bytes_per_launch = float(np.mean([s.bytes_stack for s in sets]))
     launch_s = float(stack_ms.mean()) / 1e3
     achieved = bytes_per_launch / launch_s / 1e9
+    traffic, traffic_src = pmc_traffic("vsg_stackf_kernel")
     res = {
         "metric": "vehicle-pass windows/sec -> stacked VSG + f-v images/sec; % HBM/MFMA roofline",
         "value": windows_per_step * args.steps / elapsed,
@@ -219,7 +273,7 @@ def main():
                    "parallelism": f"dp{world} (passes sharded, all-reduce of class stacks)"},
         "images_per_s": images_per_step * args.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "vsg_stackf_kernel", "bytes_per_launch": bytes_per_launch,
                      "launch_ms": launch_s * 1e3},
         "host_index_tables_s": sum(s.t_plan for s in sets),

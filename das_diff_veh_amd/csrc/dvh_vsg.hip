@@ -63,6 +63,15 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// XCD-aware block order (blocks are dealt round robin over the 8 XCDs, each with its own L2):
+// consecutive logical blocks -- the row tasks of one pass chunk, which all read that chunk's pivot
+// channel -- run on the same XCD.  A bijection on [0, gridDim.x).
+__device__ __forceinline__ int xcd_block() {
+  const int G = gridDim.x, b = blockIdx.x;
+  const int q = G / 8, r = G % 8, x = b % 8, k = b / 8;
+  return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
 template <class E>
 __device__ __forceinline__ E make_engine(char* lds) {
   E::block_init(lds);
@@ -167,10 +176,19 @@ __device__ __forceinline__ void side_scale(int flags, const RowTask& t, float sf
 
 // Time-domain epilogue of a row: lag permutation, per-pass scales, optional row norm, two-sided
 // average -> G[m] for output lag j = lane + 64 m (post_processing_XCF + VirtualShotGather.__init__).
+// Opaque copy of a per-lane value: index arithmetic derived from it stays where it is used instead
+// of being hoisted to the kernel entry (where, for cold paths, it only occupies registers and gets
+// spilled once per wave).
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 template <class E>
 __device__ __forceinline__ void row_epilogue(const E& eng, const VsgArgs& A, const float2* Y, const RowTask& t,
-                                             float sf, float so, int lane, float (&G)[E::NJ]) {
+                                             float sf, float so, int lane_, float (&G)[E::NJ]) {
   constexpr int NJ = E::NJ;
+  const int lane = opaque(lane_);  // cold path (norms / NaN fallback): keep its index math local
   const bool other = (A.flags & kFlagOtherSide) != 0;
   const bool norm = (A.flags & kFlagNorm) != 0;
   const int w = A.w, h = w / 2;
@@ -246,7 +264,7 @@ __global__ __launch_bounds__(64 * E::kWaves, Occ<E>::v) void vsg_gather_kernel(V
   constexpr int NJ = E::NJ;
   const int64_t n_task = (int64_t)A.n_pass * A.R;
   const int64_t stride = (int64_t)gridDim.x * E::kWaves;
-  for (int64_t t = (int64_t)blockIdx.x * E::kWaves + wave; t < n_task; t += stride) {
+  for (int64_t t = (int64_t)xcd_block() * E::kWaves + wave; t < n_task; t += stride) {
     const int p = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const RowTask task = make_task(A, p, i);
     RowTask tn = task;
@@ -278,7 +296,7 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stack_kernel(V
   constexpr int NJ = E::NJ;
   const int64_t n_task = (int64_t)n_chunk * A.R;
   const int64_t stride = (int64_t)gridDim.x * E::kWaves;
-  for (int64_t t = (int64_t)blockIdx.x * E::kWaves + wave; t < n_task; t += stride) {
+  for (int64_t t = (int64_t)xcd_block() * E::kWaves + wave; t < n_task; t += stride) {
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = uni(chunk_tab[3 * c]), e = uni(chunk_tab[3 * c + 1]), slot = uni(chunk_tab[3 * c + 2]);
     // first pass of the wave's next task (for the cross-task slice prefetch)
@@ -329,7 +347,7 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
     float* __restrict__ stack) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
-  const int lane = threadIdx.x & 63;
+  const int lane_ = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -339,7 +357,7 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
   const int h = N / 2;
   const int64_t n_task = (int64_t)n_chunk * A.R;
   const int64_t stride = (int64_t)gridDim.x * E::kWaves;
-  for (int64_t t = (int64_t)blockIdx.x * E::kWaves + wave; t < n_task; t += stride) {
+  for (int64_t t = (int64_t)xcd_block() * E::kWaves + wave; t < n_task; t += stride) {
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = uni(chunk_tab[3 * c]), e = uni(chunk_tab[3 * c + 1]), slot = uni(chunk_tab[3 * c + 2]);
     int np = -1, ni = 0;
@@ -363,6 +381,8 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
       float2 Cf[NH], Co[NH];
       eng.spectra(task, tn, has_next, A.w, A.hop, Cf, Co);
       const float sf = unif(scales[2 * p]), so = unif(scales[2 * p + 1]), wp = unif(weight[p]);
+      // per-pass bin / twiddle-index math recomputed here (hoisted, it only spills)
+      const int lane = opaque(lane_);
       bool bad = false, nzo = false;
       float s2f = 0.f, s2o = 0.f;
 #pragma unroll
@@ -436,7 +456,7 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
     const float inv_n = 1.0f / (float)N;
 #pragma unroll
     for (int m = 0; m < NJ; ++m) {
-      const int j = lane + 64 * m;
+      const int j = lane_ + 64 * m;
       if (j < A.w) atomicAdd(o + j, eng.c(Y, j, A.w).x * inv_n);
     }
     wave_sync();

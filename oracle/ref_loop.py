@@ -111,3 +111,30 @@ def class_images(windows, slots, n_slot, pivot, start_x, end_x):
         cnt[s] += 1
     stacks = [a / c for a, c in zip(acc, cnt) if c]
     return stacks, [disp_image(st, gx, gt) for st in stacks]
+
+
+
+def timed_worker(path, first, budget_s):
+    """One single-threaded worker of the all-core CPU baseline: gathers of the windows saved in
+    ``path`` (.npz: wins [n, C, T] float32, x_axis, t_axis, vx/vt [n, L], pivot, start_x, end_x),
+    round robin from window ``first``, until ``budget_s`` has elapsed.  Returns (done, seconds)."""
+    import time
+    z = np.load(path, allow_pickle=False)
+    wins, vx, vt = z["wins"], z["vx"], z["vt"]
+    x_axis, t_axis = z["x_axis"], z["t_axis"]
+    pivot, start_x, end_x = float(z["pivot"]), float(z["start_x"]), float(z["end_x"])
+    n, done = wins.shape[0], 0
+    t0 = time.perf_counter()
+    while True:
+        i = (first + done) % n
+        gather(np.asarray(wins[i], np.float64), x_axis, t_axis, vx[i], vt[i], pivot, start_x, end_x)
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            return done, el
+
+
+if __name__ == "__main__":  # python -m oracle.ref_loop SAMPLE.npz FIRST BUDGET_S  -> "done seconds"
+    import sys
+    d, t = timed_worker(sys.argv[1], int(sys.argv[2]), float(sys.argv[3]))
+    print(d, t)

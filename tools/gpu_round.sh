@@ -1,10 +1,15 @@
-# One GPU session: variant A/B (+ their VSG tests), full GPU suite, bench with CPU baseline, rocprofv3 kernel stats.
+# One GPU session: full GPU test suite, bench with the CPU baseline, rocprofv3 kernel stats, PMC
+# passes.   bash tools/gpu_round.sh TAG
 set -o pipefail
-bash tools/ab.sh "$@" || exit 1
-timeout -k 10 400 python -m pytest tests -m gpu -q -x > gpurun_out/gpu_tests.log 2>&1; rc=$?; echo gpu_tests=$rc; tail -3 gpurun_out/gpu_tests.log
+tag=${1:-r1}
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
+echo gpu_tests=$rc; tail -3 gpurun_out/gpu_tests.log
 [ $rc -eq 0 ] || exit 1
-timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo bench failed; tail -5 gpurun_out/bench.err; exit 1; }
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail -5 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+bash tools/pmc.sh $tag > gpurun_out/pmc.log 2>&1 || { echo pmc failed; tail -5 gpurun_out/pmc.log; exit 1; }
+timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo bench failed; tail -5 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o r1 --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err; echo prof=$?
-find gpurun_out/prof -name "*stats*" | head
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o $tag --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err; echo prof=$?

@@ -1,12 +1,16 @@
 """Average per-dispatch PMC values of the hot-path kernels from rocprofv3 counter_collection CSVs.
 
-    python tools/pmc_summary.py <dir with p*/.../*counter_collection.csv> <out.json>
+    python tools/pmc_summary.py <dir with c*/ and p*/ .../*counter_collection.csv> <out.json>
 
 Counter values are summed over the dimensions rocprofv3 reports per dispatch, then averaged over
 the dispatches of each kernel.  HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
-WRITE_SIZE are in KiB; FETCH_SIZE is reported as-is and doubled ("fetch_bytes_x2") because gfx950
-tallies 128-B requests at 64 B for wide streaming reads (the correction is calibrated only for
-16-B-per-lane loads; our loads are 4 B per lane, so both figures are kept).
+WRITE_SIZE are in KiB, and FETCH_SIZE is exact only after a per-access-width correction (gfx950
+tallies wide streaming reads at half).  The correction is measured here, not assumed: the
+calibration program tools/calib/fetch_calib streams 1 GiB with 4-byte-per-lane loads (the VSG
+kernels' sub-window loads), 1 GiB with 16-byte-per-lane loads and 256 MiB of 4-byte float atomics;
+"calibration" holds bytes / counter bytes for each, and every kernel's "traffic_bytes" is
+FETCH_SIZE x the 4-byte read factor + WRITE_SIZE x the atomic factor (its stores are float atomics
+and scratch).
 """
 import csv
 import glob
@@ -16,7 +20,8 @@ import sys
 from collections import defaultdict
 
 KERNELS = ("vsg_stackf_kernel", "vsg_stack_kernel", "vsg_scales_kernel", "tdft_gemm_kernel", "fk_contract_kernel",
-           "fv_kernel")
+           "fv_kernel", "read4", "read16", "atomic4")
+CALIB_BYTES = {"read4": ("FETCH_SIZE", 1 << 30), "read16": ("FETCH_SIZE", 1 << 30), "atomic4": ("WRITE_SIZE", 256 << 20)}
 
 
 def main():
@@ -46,9 +51,21 @@ def main():
         if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:
             d["valu_per_wave"] = d["SQ_INSTS_VALU"] / max(d["SQ_WAVES"], 1)
         res[k] = d
+    calib = {}
+    for k, (ctr, nbytes) in CALIB_BYTES.items():
+        if k in res and ctr in res[k] and res[k][ctr] > 0:
+            calib[k] = nbytes / (res[k][ctr] * 1024.0)
+    if calib:
+        res["calibration"] = calib
+        f4, fa = calib.get("read4"), calib.get("atomic4")
+        for k, d in res.items():
+            if k in CALIB_BYTES or k == "calibration" or f4 is None or fa is None:
+                continue
+            if "fetch_bytes" in d and "write_bytes" in d:
+                d["traffic_bytes"] = d["fetch_bytes"] * f4 + d["write_bytes"] * fa
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
-    print(json.dumps({k: {c: v for c, v in d.items() if not c.endswith("_dispatches")} for k, d in res.items()},
+    print(json.dumps({k: {c: v for c, v in d.items() if not str(c).endswith("_dispatches")} for k, d in res.items()},
                      indent=1))
 
 
