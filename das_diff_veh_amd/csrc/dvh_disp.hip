@@ -147,7 +147,8 @@ __global__ __launch_bounds__(256) void fk_contract_kernel(const double* __restri
 
 // ---------------------------------------------------------------------------------------------
 // 3. f-v sampling + Savitzky-Golay.  One block = (gather b, 16 velocity rows), all frequencies.
-constexpr int kVC = 16;
+constexpr int kVC = 4;        // velocities per block: 750 blocks for one set of 3 images of 1000 x 242
+constexpr int kVS = kVC + 1;  // LDS row stride: the f-consecutive FIR reads hit distinct banks
 
 __global__ __launch_bounds__(256) void fv_kernel(const double* __restrict__ FK, int32_t n_kb, int32_t n_fb,
                                                   const double* __restrict__ kgrid, double kmin, double kmax,
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(256) void fv_kernel(const double* __restrict__ FK, 
                                                   const int32_t* __restrict__ fj, const double* __restrict__ fw,
                                                   const double* __restrict__ sg, int32_t sgl,
                                                   float* __restrict__ fv) {
-  extern __shared__ __attribute__((aligned(16))) float raw[];  // [nF][kVC]
+  extern __shared__ __attribute__((aligned(16))) float raw[];  // [nF][kVS]
   const int b = blockIdx.y, v0 = blockIdx.x * kVC;
   const double* F = FK + (int64_t)b * n_kb * n_fb;
   const double k0 = kgrid[0], inv_dk = 1.0 / (kgrid[1] - kgrid[0]);
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(256) void fv_kernel(const double* __restrict__ FK, 
       const double z10 = F[(m + 1) * n_fb + j], z11 = F[(m + 1) * n_fb + j + 1];
       val = (float)(z00 * hx0 * hy0 + z01 * hx0 * hy1 + z10 * hx1 * hy0 + z11 * hx1 * hy1);
     }
-    raw[f * kVC + iv] = val;
+    raw[f * kVS + iv] = val;
   }
   __syncthreads();
   const int half = sgl / 2;
@@ -190,12 +191,12 @@ __global__ __launch_bounds__(256) void fv_kernel(const double* __restrict__ FK, 
     if (v >= nV) continue;
     double acc = 0.0;
     if (f < half) {
-      for (int t = 0; t < sgl; ++t) acc += el[f * sgl + t] * (double)raw[t * kVC + iv];
+      for (int t = 0; t < sgl; ++t) acc += el[f * sgl + t] * (double)raw[t * kVS + iv];
     } else if (f >= nF - half) {
       const int r = f - (nF - half);
-      for (int t = 0; t < sgl; ++t) acc += er[r * sgl + t] * (double)raw[(nF - sgl + t) * kVC + iv];
+      for (int t = 0; t < sgl; ++t) acc += er[r * sgl + t] * (double)raw[(nF - sgl + t) * kVS + iv];
     } else {
-      for (int t = 0; t < sgl; ++t) acc += h[t] * (double)raw[(f - half + t) * kVC + iv];
+      for (int t = 0; t < sgl; ++t) acc += h[t] * (double)raw[(f - half + t) * kVS + iv];
     }
     fv[((int64_t)b * nV + v) * nF + f] = (float)acc;
   }
@@ -281,7 +282,7 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
   if (n_kb < 2 || n_fb < 2) return set_error(-2, "FK grid needs at least 2 x 2 bins");
   if (sgl % 2 == 0 || sgl > nF) return set_error(-4, "savgol window must be odd and <= number of frequencies");
   if (B <= 0 || nV <= 0) return 0;
-  const size_t lds = sizeof(float) * (size_t)nF * kVC;
+  const size_t lds = sizeof(float) * (size_t)nF * kVS;
   if (lds > 160 * 1024) return set_error(-4, "too many frequencies for one block");
   hipError_t e = hipFuncSetAttribute((const void*)fv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
