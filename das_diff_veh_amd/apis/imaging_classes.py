@@ -1,9 +1,10 @@
-"""Per-class imaging orchestration — drop-in for apis/imaging_classes.py:87-141 of the reference.
+"""Per-class imaging orchestration — drop-in for apis/imaging_classes.py:8-48, 87-141 of the reference.
 
 ``get_images`` no longer loops over passes in Python: every window of the list goes to the device in
 one batch, the class mean is produced by the fused correlate-and-stack kernel
 (``dvh_vsg_stack``), and ``self.images`` (the per-pass gathers) is materialised lazily, in one
-batched launch, only if a caller touches it.
+batched launch, only if a caller touches it.  ``bootstrap_disp`` (and the notebooks' ``convergence_test``) run every
+resample as one device batch over gathers computed once (das_diff_veh_amd.bootstrap).
 """
 from __future__ import annotations
 
@@ -90,3 +91,32 @@ class VirtualShotGathersFromWindows(ImagesFromWindows):
         avg = stack[0].detach().to("cpu").numpy().astype(np.float64)
         self.avg_image = VirtualShotGather._from_arrays(windows[0], avg, geoms[0].gather_x_axis,
                                                         geoms[0].gather_t_axis)
+
+
+def bootstrap_disp(surf_wins, bt_size, bt_times, sigma, pivot, start_x, end_x, ref_freq_idx, freq_lb, freq_up,
+                   ref_vel):
+    """apis/imaging_classes.py:8-48: bt_times resamples of random.sample(range(1, n), bt_size)
+    windows -> class-stack VSG -> compute_disp_image(end_x=0, start_x=-150) -> one ridge per mode.
+    Same draws (Python ``random``), same return value: (ridge_vel[mode][resample], freqs).  All
+    resamples run as one batch on the device (das_diff_veh_amd.bootstrap)."""
+    from .. import bootstrap as bt
+    cache = bt.GatherCache(surf_wins, pivot, start_x, end_x)
+    sels = bt.draw(len(surf_wins), bt_size, bt_times)
+    per_mode = bt.bootstrap_ridges(cache, sels, sigma, ref_freq_idx, freq_lb, freq_up, ref_vel)
+    return [list(r) for r in per_mode], bt.FREQS.copy()
+
+
+def convergence_test(max_sample_num, windows, bt_times, sigma, x0, start_x, end_x, ref_freq_idx, freq_lb, freq_ub,
+                     vel_ref):
+    """imaging_diff_speed.ipynb#cell30: for bt_size = 1..max_sample_num, the summed per-frequency
+    std of the bootstrap ridges -> [n_modes, max_sample_num].  The gathers are computed once for all
+    60 x bt_times resamples (the notebook recomputes them per resample); draws as the notebook's."""
+    from .. import bootstrap as bt
+    cache = bt.GatherCache(windows, x0, start_x, end_x)
+    out = np.empty((len(freq_lb), max_sample_num))
+    for bt_size in range(1, max_sample_num + 1):
+        sels = bt.draw(len(windows), bt_size, bt_times)
+        per_mode = bt.bootstrap_ridges(cache, sels, sigma, ref_freq_idx, freq_lb, freq_ub, vel_ref)
+        for m, r in enumerate(per_mode):
+            out[m, bt_size - 1] = np.sum(np.std(r, axis=0))
+    return out

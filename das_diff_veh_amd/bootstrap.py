@@ -1,0 +1,150 @@
+"""Bootstrap / convergence resampling on the device.
+
+The reference recomputes every virtual shot gather of every resample from scratch
+(``bootstrap_disp``, apis/imaging_classes.py:8-48, called 30 x 60 times per class by the notebooks'
+``convergence_test``, imaging_diff_speed.ipynb#cell30).  Here:
+
+  1. the per-pass gathers of all windows are computed once (``dvh_vsg_gathers``) and kept in HBM
+     (``GatherCache``; 96 KB per pass for the notebook geometry);
+  2. a resample's stack -- ``sum(images) / len(images)`` of its ``random.sample`` draw -- is a gather-
+     mean over the cached rows the dispersion image reads (``dvh_select_mean``, summed in draw order);
+  3. the f-v images of all resamples go through the batched dispersion kernels in one launch each;
+  4. every (resample, mode) ridge is walked by one wave (``dvh_ridge``): extract_ridge_ref_idx,
+     modules/utils.py:621-678, with its strict velocity window, first-index argmax and savgol(25, 2).
+
+Random draws use Python's ``random`` exactly as the reference does (``random.sample(range(1, n), k)``,
+index 0 never drawn), so seeding ``random`` reproduces the reference's resamples.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import torch
+
+from . import _lib
+from .device import default_device, to_device_f32
+from .disp import DispPlan, fk_grid, fv_from_fk, savgol_operator
+from .plan import VsgParams, VsgPlan, pass_geometry
+from .vsg import vsg_gathers
+
+FREQS = np.arange(0.8, 25, 0.1)   # Dispersion defaults of compute_disp_image (apis/virtual_shot_gather.py:247)
+VELS = np.arange(200, 1200)
+_SG_RIDGE = None
+
+
+def _sg_ridge():
+    global _SG_RIDGE
+    if _SG_RIDGE is None:
+        h, el, er = savgol_operator(25, 2)
+        _SG_RIDGE = np.concatenate([h, el.ravel(), er.ravel()])
+    return _SG_RIDGE
+
+
+def ridges(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25, vel_max=400, ref_vel=None):
+    """extract_ridge_ref_idx (modules/utils.py:621-678) for every image of ``fv`` [B, Nvel, Nfreq]
+    (device float32, rows in the map's order = ``vels`` reversed) on the band lb <= f < ub.
+    ``ref_freq_idx`` indexes the band; ``ref_vel`` is a callable of frequency (or an array over
+    the band).  Returns float64 [B, n_band] on the host."""
+    if not isinstance(fv, torch.Tensor) or not fv.is_cuda or fv.dtype != torch.float32 or fv.dim() != 3:
+        raise ValueError("fv must be a float32 device tensor [B, Nvel, Nfreq] (no CPU fallback)")
+    freqs = np.asarray(freqs, dtype=np.float64)
+    vel_desc = np.asarray(vels, dtype=np.float64)[::-1].copy()
+    fv = fv.contiguous()  # rows [Nvel][Nfreq] as the kernel indexes them
+    if vel_desc.size != fv.shape[1] or freqs.size != fv.shape[2]:
+        raise ValueError("fv shape does not match (vels, freqs)")
+    if vel_desc.size > 1 and not np.all(np.diff(vel_desc) < 0):
+        raise ValueError("the device ridge walk needs strictly increasing vels")
+    band = np.flatnonzero((freqs >= freq_lb) & (freqs < freq_ub))
+    if band.size == 0:
+        raise ValueError("empty frequency band")
+    if not np.array_equal(band, np.arange(band[0], band[-1] + 1)):
+        raise ValueError("the frequency band must be contiguous")
+    c0, nb = int(band[0]), int(band.size)
+    dev = fv.device
+    vref = None
+    if ref_freq_idx is not None and ref_vel is not None:
+        vr = ref_vel(freqs[band]) if callable(ref_vel) else np.asarray(ref_vel, dtype=np.float64)
+        vref = torch.as_tensor(np.asarray(vr, dtype=np.float64).reshape(nb), device=dev)
+    ref = -1 if ref_freq_idx is None else int(ref_freq_idx)
+    if ref_freq_idx is not None and not 0 <= ref < nb:
+        raise IndexError(f"index {ref} is out of bounds for axis 0 with size {nb}")
+    B = fv.shape[0]
+    out = torch.empty((B, nb), dtype=torch.float64, device=dev)
+    status = torch.zeros(B, dtype=torch.int32, device=dev)
+    vel_t = torch.as_tensor(vel_desc, device=dev)
+    sg = torch.as_tensor(_sg_ridge(), device=dev)
+    _lib.call("dvh_ridge", _lib.ptr(fv), fv.stride(0), B, fv.shape[1], fv.shape[2], c0, nb, _lib.ptr(vel_t), ref,
+              float(sigma), float(vel_max), _lib.ptr(vref), _lib.ptr(sg), 25, _lib.ptr(out), _lib.ptr(status),
+              _lib.stream_of(dev))
+    if int(status.max()) != 0:
+        raise ValueError("attempt to get argmax of an empty sequence (no velocity inside a ridge window)")
+    return out.cpu().numpy()
+
+
+class GatherCache:
+    """Per-pass gathers [n, R, w] of a window list on the device, computed once
+    (VirtualShotGathersFromWindows.get_images' per-pass images: norm=False, two-sided)."""
+
+    def __init__(self, windows, pivot, start_x, end_x, wlen=2, include_other_side=True, device=None):
+        self.device = device or default_device()
+        self.prm = VsgParams(pivot=pivot, start_x=start_x, end_x=end_x, wlen=wlen, norm=False,
+                             include_other_side=include_other_side)
+        geoms = [pass_geometry(w.x_axis, w.t_axis, w.veh_state_x, w.veh_state_t, self.prm) for w in windows]
+        shapes = {tuple(np.shape(w.data)) for w in windows}
+        if len(shapes) != 1:
+            raise ValueError("bootstrap windows must share one shape")
+        n_ch, n_t = shapes.pop()
+        self.plan = VsgPlan(geoms, self.prm, n_ch, n_t)
+        data = to_device_f32([w.data for w in windows], self.device)
+        self.G = vsg_gathers(data, self.plan)  # [n, R, w]
+        self.gx, self.gt = geoms[0].gather_x_axis, geoms[0].gather_t_axis
+        self.n = len(windows)
+        self._disp = {}
+
+    def disp_plan(self, start_x=-150, end_x=0, freqs=FREQS, vels=VELS):
+        """compute_disp_image's nearest-offset channel slice and its DispPlan (dx = 8.16, :247-258)."""
+        s = int(np.abs(self.gx - start_x).argmin())
+        e = int(np.abs(self.gx - end_x).argmin())
+        key = (s, e, id(freqs), id(vels))
+        if key not in self._disp:
+            dt = self.gt[1] - self.gt[0]
+            self._disp[key] = (s, e, DispPlan(e + 1 - s, self.plan.w, 8.16, dt, freqs, vels))
+        return self._disp[key]
+
+    def resample_stacks(self, sel, start_x=-150, end_x=0):
+        """Mean gathers over the disp rows for every draw: sel [B, k] pass indices -> [B, nch, w]."""
+        sel = np.asarray(sel, dtype=np.int32)
+        if sel.ndim != 2 or sel.size == 0 or sel.min() < 0 or sel.max() >= self.n:
+            raise ValueError("selections must be [B, k] pass indices")
+        s, e, _ = self.disp_plan(start_x, end_x)
+        w, R = self.plan.w, self.plan.R
+        B, k = sel.shape
+        out = torch.empty((B, e + 1 - s, w), dtype=torch.float32, device=self.device)
+        sel_t = torch.as_tensor(sel, device=self.device)
+        base = self.G[:, s:e + 1, :]
+        _lib.call("dvh_select_mean", _lib.ptr(base), R * w, (e + 1 - s) * w, _lib.ptr(sel_t), B, k, _lib.ptr(out),
+                  (e + 1 - s) * w, _lib.stream_of(self.device))
+        return out
+
+    def resample_images(self, sel, start_x=-150, end_x=0):
+        """f-v images [B, Nvel, Nfreq] of every draw's stack (compute_disp_image(end_x, start_x))."""
+        _, _, plan = self.disp_plan(start_x, end_x)
+        return fv_from_fk(fk_grid(self.resample_stacks(sel, start_x, end_x), plan), plan)
+
+
+def bootstrap_ridges(cache: GatherCache, sels, sigma, ref_freq_idx, freq_lb, freq_up, ref_vel, start_x=-150,
+                     end_x=0):
+    """Ridge velocities per mode for draws ``sels`` [B, k]: list over modes of [B, n_band] arrays."""
+    fv = cache.resample_images(sels, start_x, end_x)
+    out = []
+    for m in range(len(freq_lb)):
+        ref = ref_freq_idx[m] - int(np.sum(FREQS < freq_lb[m]))
+        out.append(ridges(fv, FREQS, VELS, freq_lb[m], freq_up[m], ref_freq_idx=ref, sigma=sigma[m], vel_max=800,
+                          ref_vel=ref_vel[m]))
+    return out
+
+
+def draw(n, bt_size, bt_times, rand=random):
+    """The reference's draws: bt_times x random.sample(range(1, n), bt_size)."""
+    return np.array([rand.sample(range(1, n), bt_size) for _ in range(bt_times)], dtype=np.int32)

@@ -1,0 +1,239 @@
+// Bootstrap / convergence resampling on MI355X (gfx950): SURVEY §8(f) row 1.
+//
+// Replaces, for all resamples of a bootstrap run at once:
+//   bootstrap_disp                 apis/imaging_classes.py:8-48 (per resample: VSG stack of
+//                                  random.sample(range(1, n), bt_size) windows, compute_disp_image,
+//                                  extract_ridge_ref_idx per mode)
+//   extract_ridge_ref_idx          modules/utils.py:621-678
+// The per-pass gathers are computed once (dvh_vsg_gathers); a resample's stack is the mean of its
+// selected gathers (select_mean_kernel); the f-v images of all resamples run through the batched
+// dispersion kernels (dvh_disp_*); ridge_kernel walks every (resample, mode) ridge in one wave.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "dvh_common.h"
+#include "dvh.h"
+
+namespace dvh {
+
+// out[b][k] = (sum_{j < m} G[sel[b][j]][k]) / m over the contiguous K-element block of each pass,
+// summed in selection order (the reference's sum(images) / len(images)).  float4 per lane.
+__global__ __launch_bounds__(256) void select_mean_kernel(const float* __restrict__ G, int64_t pass_stride, int64_t K,
+                                                          const int32_t* __restrict__ sel, int32_t m,
+                                                          float* __restrict__ out, int64_t out_stride) {
+  const int b = blockIdx.y;
+  const int32_t* s = sel + (int64_t)b * m;
+  const bool vec = (K % 4 == 0) && (pass_stride % 4 == 0) && (out_stride % 4 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(G) | reinterpret_cast<uintptr_t>(out)) % 16 == 0);
+  if (vec) {
+    const int64_t k4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (4 * k4 >= K) return;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < m; ++j) {
+      const float4 g = reinterpret_cast<const float4*>(G + (int64_t)s[j] * pass_stride)[k4];
+      acc.x += g.x;
+      acc.y += g.y;
+      acc.z += g.z;
+      acc.w += g.w;
+    }
+    // divide (not multiply by 1/m): sum / len as the reference evaluates it
+    reinterpret_cast<float4*>(out + (int64_t)b * out_stride)[k4] =
+        make_float4(acc.x / (float)m, acc.y / (float)m, acc.z / (float)m, acc.w / (float)m);
+  } else {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += (int64_t)gridDim.x * blockDim.x) {
+      float acc = 0.f;
+      for (int j = 0; j < m; ++j) acc += G[(int64_t)s[j] * pass_stride + k];
+      out[(int64_t)b * out_stride + k] = acc / (float)m;
+    }
+  }
+}
+
+// np.argmax order over (value, row): a NaN beats any number, the first row wins ties
+__device__ __forceinline__ bool better(float a, int ra, float b, int rb) {
+  const bool na = isnan(a), nb = isnan(b);
+  if (na != nb) return na;
+  if (na || a == b) return ra < rb;
+  return a > b;
+}
+
+__device__ __forceinline__ void wave_argmax(float& v, int& r) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(v, o);
+    const int r2 = __shfl_xor(r, o);
+    if (r2 >= 0 && (r < 0 || better(v2, r2, v, r))) {
+      v = v2;
+      r = r2;
+    }
+  }
+}
+
+// first row r (of nV, velocities descending) with vel[r] < x: rows [0, r) have vel >= x
+__device__ __forceinline__ int first_below(const double* __restrict__ vel, int nV, double x) {
+  int lo = 0, hi = nV;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (vel[mid] < x) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+// first row r with vel[r] <= x
+__device__ __forceinline__ int first_at_or_below(const double* __restrict__ vel, int nV, double x) {
+  int lo = 0, hi = nV;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (vel[mid] <= x) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+// argmax of column c over rows [r0, r1) (first max wins); -1 when the range is empty
+__device__ __forceinline__ int column_argmax(const float* __restrict__ F, int nF, int c, int r0, int r1, int lane) {
+  float best = 0.f;
+  int row = -1;
+  for (int r = r0 + lane; r < r1; r += 64) {
+    const float v = F[(int64_t)r * nF + c];
+    if (row < 0 || better(v, r, best, row)) {
+      best = v;
+      row = r;
+    }
+  }
+  wave_argmax(best, row);
+  return row;
+}
+
+constexpr int kMaxBand = 1024;
+
+// One wave per (image b, ridge):  extract_ridge_ref_idx (modules/utils.py:621-678) on the band of
+// columns [c0, c0 + nb) of fv[b] ([nV][nF], rows = velocities in descending order vel[r]).
+//   ref < 0:  vel_max mode, raw picks over rows at/after argmin |vel_max - vel| (no smoothing)
+//   vref:     per-column reference velocities (ref_vel(freq)), window (vref - sigma, vref + sigma)
+//   else:     pick at column ref over all rows, then walk backward / forward with the window
+//             (v_prev - sigma, v_prev + sigma); savgol(sgl, 2, mode='interp') of the picks.
+// status[b] = 0, or 1 when a window holds no velocity (np.argmax of an empty slice raises).
+__global__ __launch_bounds__(64) void ridge_kernel(const float* __restrict__ fv, int64_t b_stride, int32_t nV,
+                                                   int32_t nF, int32_t c0, int32_t nb, const double* __restrict__ vel,
+                                                   int32_t ref, double sigma, double vel_max,
+                                                   const double* __restrict__ vref, const double* __restrict__ sg,
+                                                   int32_t sgl, double* __restrict__ out, int32_t* __restrict__ status) {
+  __shared__ double pick[kMaxBand];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const float* F = fv + (int64_t)b * b_stride;
+  double* o = out + (int64_t)b * nb;
+  int err = 0;
+  if (ref < 0) {
+    // max_idx = argmin |vel_max - vel| (first of equal distances)
+    double bd = INFINITY;
+    int bi = nV;
+    for (int r = lane; r < nV; r += 64) {
+      const double d = fabs(vel_max - vel[r]);
+      if (d < bd || (d == bd && r < bi)) {
+        bd = d;
+        bi = r;
+      }
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+      const double d2 = __shfl_xor(bd, s);
+      const int i2 = __shfl_xor(bi, s);
+      if (d2 < bd || (d2 == bd && i2 < bi)) {
+        bd = d2;
+        bi = i2;
+      }
+    }
+    for (int i = 0; i < nb; ++i) {
+      const int r = column_argmax(F, nF, c0 + i, bi, nV, lane);
+      if (lane == 0) o[i] = r >= 0 ? vel[r] : NAN;
+      err |= r < 0;
+    }
+    if (lane == 0) status[b] = err;
+    return;
+  }
+  if (vref) {
+    for (int i = 0; i < nb; ++i) {
+      const int r0 = first_below(vel, nV, vref[i] + sigma), r1 = first_at_or_below(vel, nV, vref[i] - sigma);
+      const int r = column_argmax(F, nF, c0 + i, r0, r1, lane);
+      err |= r < 0;
+      if (lane == 0) pick[i] = r >= 0 ? vel[r] : NAN;
+    }
+  } else {
+    const int rr = column_argmax(F, nF, c0 + ref, 0, nV, lane);
+    const double vr = rr >= 0 ? vel[rr] : NAN;  // wave-uniform (every lane holds the reduced row)
+    double v = vr;
+    if (lane == 0) pick[ref] = v;
+    for (int i = ref - 1; i >= 0; --i) {  // backward
+      const int r0 = first_below(vel, nV, v + sigma), r1 = first_at_or_below(vel, nV, v - sigma);
+      const int r = column_argmax(F, nF, c0 + i, r0, r1, lane);
+      err |= r < 0;
+      v = r >= 0 ? vel[r] : NAN;
+      if (lane == 0) pick[i] = v;
+    }
+    v = vr;
+    for (int i = ref + 1; i < nb; ++i) {  // forward
+      const int r0 = first_below(vel, nV, v + sigma), r1 = first_at_or_below(vel, nV, v - sigma);
+      const int r = column_argmax(F, nF, c0 + i, r0, r1, lane);
+      err |= r < 0;
+      v = r >= 0 ? vel[r] : NAN;
+      if (lane == 0) pick[i] = v;
+    }
+  }
+  __syncthreads();
+  // savgol_filter(picks, sgl, 2) with mode='interp': interior taps h, edge fits el / er
+  const int half = sgl / 2;
+  const double* h = sg;
+  const double* el = sg + sgl;
+  const double* er = el + half * sgl;
+  for (int i = lane; i < nb; i += 64) {
+    double acc = 0.0;
+    if (i < half) {
+      for (int t = 0; t < sgl; ++t) acc += el[i * sgl + t] * pick[t];
+    } else if (i >= nb - half) {
+      for (int t = 0; t < sgl; ++t) acc += er[(i - (nb - half)) * sgl + t] * pick[nb - sgl + t];
+    } else {
+      for (int t = 0; t < sgl; ++t) acc += h[t] * pick[i - half + t];
+    }
+    o[i] = acc;
+  }
+  if (lane == 0) status[b] = err;
+}
+
+static int last_launch() {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
+}
+
+}  // namespace dvh
+
+using namespace dvh;
+
+DVH_API int dvh_select_mean(const float* G, int64_t pass_stride, int64_t K, const int32_t* sel, int32_t B, int32_t m,
+                            float* out, int64_t out_stride, void* stream) {
+  if (!G || !sel || !out) return set_error(-2, "null pointer argument");
+  if (m <= 0 || K < 0 || B < 0) return set_error(-2, "invalid sizes");
+  if (B == 0 || K == 0) return 0;
+  if (B > 65535) return set_error(-4, "too many resamples for one launch");
+  const int64_t blocks = (K / 4 + 255) / 256 + 1;
+  hipLaunchKernelGGL(select_mean_kernel, dim3((unsigned)blocks, B), dim3(256), 0, (hipStream_t)stream, G, pass_stride,
+                     K, sel, m, out, out_stride);
+  return last_launch();
+}
+
+DVH_API int dvh_ridge(const float* fv, int64_t b_stride, int32_t B, int32_t nV, int32_t nF, int32_t c0, int32_t nb,
+                      const double* vel, int32_t ref, double sigma, double vel_max, const double* vref,
+                      const double* sg, int32_t sgl, double* out, int32_t* status, void* stream) {
+  if (!fv || !vel || !out || !status) return set_error(-2, "null pointer argument");
+  if (nb <= 0 || c0 < 0 || c0 + nb > nF || nV <= 0) return set_error(-2, "invalid band");
+  if (nb > kMaxBand) return set_error(-4, "band longer than 1024 frequencies");
+  if (ref >= 0 || vref) {
+    if (!sg || sgl % 2 == 0 || sgl > nb) return set_error(-4, "savgol window must be odd and <= the band length");
+    if (ref >= nb) return set_error(-2, "reference index outside the band");
+  }
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(ridge_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, fv, b_stride, nV, nF, c0, nb, vel,
+                     ref, sigma, vel_max, vref, sg, sgl, out, status);
+  return last_launch();
+}

@@ -4,6 +4,8 @@
   map_fv        modules/utils.py:457-475  -> dvh_disp_tdft / dvh_disp_fk / dvh_disp_fv
   Dispersion    modules/utils.py:383-426  (same constructor, attributes, npz format, arithmetic)
   bandpass_data modules/utils.py:179-189  -> dvh_sosfiltfilt (zero-phase order-10 Butterworth)
+  extract_ridge_ref_idx modules/utils.py:621-678 -> dvh_ridge (one wave per ridge)
+  disp_curve_stats  the statistics of plot_disp_curves (:680-713), without the figure
 Host arrays in, host arrays out, like the reference; device tensors are accepted too.
 """
 from __future__ import annotations
@@ -109,3 +111,28 @@ def bandpass_data(data, dt, flo, fhi):
     """In-place zero-phase Butterworth bandpass (order 10, SOS) along time, on device."""
     from ..preprocess import bandpass_inplace
     bandpass_inplace(data, dt, flo, fhi)
+
+
+def extract_ridge_ref_idx(freq, vel, fv_map, ref_freq_idx=None, sigma=25, vel_max=400, ref_vel=None):
+    """modules/utils.py:621-678 (fv_map [Nvel, Nfreq] with rows in vel[::-1] order), walked on the
+    device by dvh_ridge (das_diff_veh_amd.bootstrap.ridges)."""
+    import torch
+
+    from ..bootstrap import ridges
+    fv = torch.as_tensor(np.ascontiguousarray(fv_map, dtype=np.float32), device=default_device())[None]
+    freq = np.asarray(freq, dtype=np.float64)
+    out = ridges(fv, freq, vel, freq[0], np.nextafter(freq[-1], np.inf), ref_freq_idx=ref_freq_idx, sigma=sigma,
+                 vel_max=vel_max, ref_vel=ref_vel)[0]
+    return out
+
+
+def disp_curve_stats(freqs, freq_lb, freq_up, ridge_vels):
+    """The statistics of plot_disp_curves (modules/utils.py:680-713) without the figure:
+    per mode the mean, range (max - min) and std over resamples of the ridge velocities."""
+    means, ranges, stds = [], [], []
+    for i in range(len(ridge_vels)):
+        rv = np.array([d for d in ridge_vels[i]], dtype=np.float64)
+        means.append(np.mean(rv, axis=0))
+        stds.append(np.std(rv, axis=0))
+        ranges.append(np.max(rv, axis=0) - np.min(rv, axis=0))
+    return means, ranges, stds

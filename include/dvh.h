@@ -97,6 +97,25 @@ int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, const d
                 double kmax, const double* kq, int32_t nF, int32_t nV, const int32_t* fj, const double* fw,
                 const double* sg, int32_t sgl, float* fv, void* stream);
 
+/* ---------------------------------------------------------------- bootstrap / convergence
+ * bootstrap_disp (apis/imaging_classes.py:8-48): per-pass gathers once, then per resample the mean
+ * stack, its f-v image (dvh_disp_*) and the ridge picks (extract_ridge_ref_idx, modules/utils.py:621-678). */
+
+/* out[b][k] = (sum_{j < m} G[sel[b * m + j] * pass_stride + k]) / m for k < K, summed in selection
+ * order (sum(images) / len(images), apis/imaging_classes.py:106-107). */
+int dvh_select_mean(const float* G, int64_t pass_stride, int64_t K, const int32_t* sel, int32_t B, int32_t m,
+                    float* out, int64_t out_stride, void* stream);
+
+/* extract_ridge_ref_idx on the frequency band [c0, c0 + nb) of fv[b] ([nV][nF], b_stride elements
+ * apart), rows = velocities vel[nV] strictly descending.  ref < 0: vel_max mode (raw picks below
+ * argmin |vel_max - vel|); vref (nullable, [nb]): per-frequency reference velocities; otherwise
+ * the walk from column ref with the window (v - sigma, v + sigma).  Picks of the last two modes are
+ * smoothed by savgol(sgl, 2) given as sg = {h[sgl], left[sgl/2][sgl], right[sgl/2][sgl]}.
+ * out[B][nb] float64; status[b] = 1 when a window held no velocity (the reference raises). */
+int dvh_ridge(const float* fv, int64_t b_stride, int32_t B, int32_t nV, int32_t nF, int32_t c0, int32_t nb,
+              const double* vel, int32_t ref, double sigma, double vel_max, const double* vref, const double* sg,
+              int32_t sgl, double* out, int32_t* status, void* stream);
+
 /* ---------------------------------------------------------------- preprocessing
  * dtype: 0 float32, 1 float64; data modified in place. */
 

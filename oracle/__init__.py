@@ -19,4 +19,5 @@ Modules:
   disp       -- map_fv / fk restatement (FK grid, bilinear clamp, Savitzky-Golay)
   preprocess -- bandpass_data (sosfiltfilt), mute_along_traj / mute_along_time
   ref_loop   -- CPU baseline that keeps the reference's per-row scipy.signal.correlate loop
+  ridge      -- extract_ridge_ref_idx and bootstrap_disp restatements (bootstrap / convergence)
 """

@@ -235,11 +235,50 @@ def gen_bandpass(ref):
     return dict(q=q, dt=np.array(0.004), out_1p2_30=y, out_0p08_1=y2)
 
 
-def main():
+def gen_ridge(ref):
+    """extract_ridge_ref_idx (modules/utils.py:621-678) on the vsg_w500 class image, and
+    bootstrap_disp (apis/imaging_classes.py:8-48) with random.seed fixed, on the 5 fixture passes."""
+    import random
+    kw = dict(pivot=700, start_x=500, end_x=900, wlen=2)
+    passes = [synth_pass(100 + i) for i in range(5)]
+    wins = [ref_window(ref, p) for p in passes]
+    images = ref.ic.VirtualShotGathersFromWindows(wins)
+    images.get_images(include_other_side=True, **kw)
+    images.avg_image.compute_disp_image(end_x=0, start_x=-200)
+    d = images.avg_image.disp
+    freqs, vels, fv = d.freqs, d.vels, d.fv_map
+    out = dict(fv_map=fv, freqs=freqs, vels=vels)
+    m0 = (freqs >= 2.5) & (freqs < 14)
+    out["walk"] = ref.ut.extract_ridge_ref_idx(freqs[m0], vels, fv[:, m0], ref_freq_idx=80 - int(np.sum(freqs < 2.5)),
+                                                sigma=25, vel_max=800)
+    m1 = (freqs >= 10) & (freqs < 15)
+    mode1 = scipy.interpolate.interp1d([10, 12, 13, 14, 15, 16], [530, 470, 450, 430, 410, 391])
+    out["refvel"] = ref.ut.extract_ridge_ref_idx(freqs[m1], vels, fv[:, m1], ref_freq_idx=130 - int(np.sum(freqs < 10)),
+                                                  sigma=50, vel_max=800, ref_vel=mode1)
+    out["refvel_f"] = np.array([10, 12, 13, 14, 15, 16], float)
+    out["refvel_v"] = np.array([530, 470, 450, 430, 410, 391], float)
+    out["velmax"] = ref.ut.extract_ridge_ref_idx(freqs[m0], vels, fv[:, m0], sigma=25, vel_max=800)
+    # bootstrap: two modes (a walk and a reference-curve mode), bt_size 3 of the 4 drawable passes
+    random.seed(11)
+    rv, fq = ref.ic.bootstrap_disp(wins, 3, 4, [25, 50], 700, 500, 900, [80, 130], [2.5, 10], [14, 15], [None, mode1])
+    out["boot_mode0"] = np.stack(rv[0])
+    out["boot_mode1"] = np.stack(rv[1])
+    out["boot_freqs"] = fq
+    random.seed(11)
+    out["boot_sel"] = np.array([random.sample(range(1, len(wins)), 3) for _ in range(4)])
+    return out
+
+
+GENERATORS = {"vsg_w500": gen_vsg, "vsg_w499": gen_vsg_w499, "vsg_edge": gen_vsg_edge, "disp": gen_disp,
+              "bandpass": gen_bandpass, "ridge": gen_ridge}
+
+
+def main(names=None):
     ref = import_reference()
     meta = dict(numpy=np.__version__, scipy=scipy.__version__)
-    for name, fn in (("vsg_w500", gen_vsg), ("vsg_w499", gen_vsg_w499), ("vsg_edge", gen_vsg_edge),
-                     ("disp", gen_disp), ("bandpass", gen_bandpass)):
+    for name, fn in GENERATORS.items():
+        if names and name not in names:
+            continue
         out = fn(ref)
         out["meta"] = np.array(repr(meta))
         path = os.path.join(HERE, f"{name}.npz")
@@ -247,5 +286,5 @@ def main():
         print(f"wrote {path}: {os.path.getsize(path) / 1e6:.2f} MB")
 
 
-if __name__ == "__main__":
-    main()
+if __name__ == "__main__":  # python tests/golden/make_golden.py [name ...]
+    main(sys.argv[1:])

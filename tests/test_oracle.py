@@ -112,3 +112,28 @@ def test_ref_loop_baseline_matches_reference():
         gs.append(x)
     fv = ref_loop.disp_image(g["stack"], g["gather_x_axis"], g["gather_t_axis"])
     assert np.abs(fv - g["fv_map"]).max() <= 1e-6 * np.abs(g["fv_map"]).max()
+
+
+def test_oracle_ridge_and_bootstrap_match_reference():
+    """oracle/ridge.py against the reference's extract_ridge_ref_idx and bootstrap_disp
+    (tests/golden/ridge.npz, random.seed(11))."""
+    import random
+
+    import scipy.interpolate
+
+    from oracle import ridge as orid
+    g = gio.load("ridge")
+    fq, vels, fv = g["freqs"], g["vels"], g["fv_map"]
+    m0, m1 = (fq >= 2.5) & (fq < 14), (fq >= 10) & (fq < 15)
+    mode1 = scipy.interpolate.interp1d(g["refvel_f"], g["refvel_v"])
+    assert np.array_equal(orid.extract_ridge_ref_idx(fq[m0], vels, fv[:, m0], ref_freq_idx=80 - int(np.sum(fq < 2.5)),
+                                                     sigma=25, vel_max=800), g["walk"])
+    assert np.array_equal(orid.extract_ridge_ref_idx(fq[m1], vels, fv[:, m1], ref_freq_idx=130 - int(np.sum(fq < 10)),
+                                                     sigma=50, vel_max=800, ref_vel=mode1), g["refvel"])
+    assert np.array_equal(orid.extract_ridge_ref_idx(fq[m0], vels, fv[:, m0], sigma=25, vel_max=800), g["velmax"])
+    v5 = gio.load("vsg_w500")
+    wins = [gio.oracle_window(v5, i) for i in range(5)]
+    random.seed(11)
+    rv, f = orid.bootstrap_disp(wins, 3, 4, [25, 50], 700, 500, 900, [80, 130], [2.5, 10], [14, 15], [None, mode1])
+    assert np.abs(np.stack(rv[0]) - g["boot_mode0"]).max() < 1e-9
+    assert np.abs(np.stack(rv[1]) - g["boot_mode1"]).max() < 1e-9
