@@ -7,6 +7,10 @@
 //   dvh_mute_traj    SurfaceWaveWindow.mute_along_traj (apis/data_classes.py:49-72): column t is
 //                    multiplied by a tukey taper placed along the vehicle trajectory (host tables).
 //   dvh_mute_time    SurfaceWaveWindow.mute_along_time (apis/data_classes.py:100-104).
+//   dvh_trace_cleanup  the rest of TimeLapseImaging._preprocessing_for_surface_waves
+//                    (apis/timeLapseImaging.py:51-71) after the bandpass: find_noise_idx /
+//                    impute_noisy_trace (modules/utils.py:316-329) for empty traces (L2 norm below
+//                    the threshold) then noisy traces (max above it), then the per-trace L2 norm.
 // Data may be float32 (dtype 0) or float64 (dtype 1), modified in place.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -111,9 +115,124 @@ static int last_launch() {
   return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
 }
 
+// ---------------------------------------------------------------------------------------------
+// Trace clean-up of the continuous record (bandpassed, [n_rows][n_t] with row_stride).
+
+constexpr int kStatBlock = 256;
+
+// NaN-propagating max (np.max returns NaN for a row holding one)
+__device__ __forceinline__ double nan_max(double a, double b) { return (isnan(a) || a > b) ? a : b; }
+
+template <typename T>
+__device__ __forceinline__ void block_row_stats(const T* __restrict__ row, int32_t n_t, double* __restrict__ out2) {
+  __shared__ double ss[kStatBlock / 64], mx[kStatBlock / 64];
+  double s = 0.0, m = -INFINITY;
+  for (int t = threadIdx.x; t < n_t; t += blockDim.x) {
+    const double v = (double)row[t];
+    s += v * v;
+    m = nan_max(m, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    m = nan_max(m, __shfl_xor(m, o));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    ss[w] = s;
+    mx[w] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = -INFINITY;
+    for (int k = 0; k < kStatBlock / 64; ++k) {
+      a += ss[k];
+      b = nan_max(b, mx[k]);
+    }
+    out2[0] = a;  // sum of squares
+    out2[1] = b;  // max
+  }
+  __syncthreads();
+}
+
+// stats[r] = {sum x^2, max x} per trace
+template <typename T>
+__global__ __launch_bounds__(kStatBlock) void row_stats_kernel(const T* __restrict__ x, int64_t row_stride,
+                                                                int32_t n_t, double* __restrict__ stats) {
+  block_row_stats(x + (int64_t)blockIdx.x * row_stride, n_t, stats + 2 * (int64_t)blockIdx.x);
+}
+
+// One find_noise_idx + impute_noisy_trace round (one block): idx = np.argmax(cond) over traces
+// (first true, 0 if none) with cond = ||x_r|| < thr (empty) or max(x_r) > thr (noisy); then
+// x[idx] = x[idx-1] (last), x[1] (first) or x[idx-1] + x[idx+1] (a sum, as the reference does);
+// the trace's stats are refreshed for the next round.
+template <typename T>
+__global__ __launch_bounds__(kStatBlock) void impute_kernel(T* __restrict__ x, int64_t n_rows, int64_t row_stride,
+                                                             int32_t n_t, int32_t empty, double thr,
+                                                             double* __restrict__ stats, int32_t* __restrict__ idx_out) {
+  __shared__ int first;
+  if (threadIdx.x == 0) first = INT32_MAX;
+  __syncthreads();
+  for (int64_t r = threadIdx.x; r < n_rows; r += blockDim.x) {
+    const bool c = empty ? (sqrt(stats[2 * r]) < thr) : (stats[2 * r + 1] > thr);
+    if (c) atomicMin(&first, (int)r);
+  }
+  __syncthreads();
+  const int64_t idx = first == INT32_MAX ? 0 : first;
+  if (threadIdx.x == 0 && idx_out) *idx_out = (int32_t)idx;
+  if (n_rows < 2) return;  // x[0] = x[-1] is x[0] itself
+  T* dst = x + idx * row_stride;
+  const T* a = x + (idx + 1 == n_rows ? idx - 1 : (idx == 0 ? 1 : idx - 1)) * row_stride;
+  const T* b = (idx > 0 && idx + 1 < n_rows) ? x + (idx + 1) * row_stride : nullptr;
+  for (int t = threadIdx.x; t < n_t; t += blockDim.x) dst[t] = b ? (T)(a[t] + b[t]) : a[t];
+  __syncthreads();
+  block_row_stats(dst, n_t, stats + 2 * idx);
+}
+
+// data /= np.linalg.norm(data, axis=-1, keepdims=True)
+template <typename T>
+__global__ __launch_bounds__(256) void row_normalize_kernel(T* __restrict__ x, int64_t row_stride, int32_t n_t,
+                                                            const double* __restrict__ stats) {
+  const int64_t r = blockIdx.y;
+  const double nrm = sqrt(stats[2 * r]);
+  T* row = x + r * row_stride;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n_t; t += gridDim.x * blockDim.x)
+    row[t] = (T)((double)row[t] / nrm);
+}
+
+template <typename T>
+static int trace_cleanup(T* x, int64_t n_rows, int64_t row_stride, int32_t n_t, int32_t flags, double thr,
+                         double* stats, int32_t* idx_out, hipStream_t s) {
+  hipLaunchKernelGGL(row_stats_kernel<T>, dim3((unsigned)n_rows), dim3(kStatBlock), 0, s, x, row_stride, n_t, stats);
+  if (flags & 1)
+    hipLaunchKernelGGL(impute_kernel<T>, dim3(1), dim3(kStatBlock), 0, s, x, n_rows, row_stride, n_t, 1, thr, stats,
+                       idx_out);
+  if (flags & 2)
+    hipLaunchKernelGGL(impute_kernel<T>, dim3(1), dim3(kStatBlock), 0, s, x, n_rows, row_stride, n_t, 0, thr, stats,
+                       idx_out ? idx_out + 1 : nullptr);
+  if (flags & 4)
+    hipLaunchKernelGGL(row_normalize_kernel<T>, dim3((unsigned)((n_t + 255) / 256), (unsigned)n_rows), dim3(256), 0,
+                       s, x, row_stride, n_t, stats);
+  return last_launch();
+}
+
 }  // namespace dvh
 
 using namespace dvh;
+
+DVH_API int dvh_trace_cleanup(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t, int32_t flags,
+                              double noise_threshold, double* stats, int32_t* idx_out, void* stream) {
+  if (!x || !stats) return set_error(-2, "null pointer argument");
+  if (n_rows <= 0 || n_t <= 0) return 0;
+  if (n_rows > 65535 && (flags & 4)) return set_error(-4, "too many traces for one launch");
+  if (dtype == 0)
+    return trace_cleanup<float>((float*)x, n_rows, row_stride, n_t, flags, noise_threshold, stats, idx_out,
+                                (hipStream_t)stream);
+  if (dtype == 1)
+    return trace_cleanup<double>((double*)x, n_rows, row_stride, n_t, flags, noise_threshold, stats, idx_out,
+                                 (hipStream_t)stream);
+  return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
+}
 
 DVH_API int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t,
                             const double* sos, int32_t n_sec, int32_t padlen, const double* zi, double* work,

@@ -7,6 +7,8 @@
                     (argmax(x > car(t) - offset/2 + delta_x), clipped) is tabulated on the host with
                     the reference's float64 expressions; the multiply runs in dvh_mute_traj
   mute_along_time   apis/data_classes.py:100-104 -> dvh_mute_time
+  surface_wave_preprocessing  TimeLapseImaging._preprocessing_for_surface_waves (apis/timeLapseImaging.py:
+                    51-71): bandpass + empty / noisy trace imputation + per-trace L2 norm
 """
 from __future__ import annotations
 
@@ -115,3 +117,34 @@ def mute_along_time(window, alpha=0.3):
     _lib.call("dvh_mute_time", _lib.ptr(v.t), v.dtype, v.t.numel() // n_t, n_t, _lib.ptr(taper_t),
               _lib.stream_of(dev))
     v.write_back()
+
+
+def surface_wave_preprocessing(data, dt, method="surface_wave", flo=1.2, fhi=30, impute_noise_traces=True,
+                               noise_threshold=5, impute_empty_traces=True, return_indices=False):
+    """TimeLapseImaging._preprocessing_for_surface_waves (apis/timeLapseImaging.py:51-71) of a
+    continuous record [n_ch, n_t] -> ``data_for_imaging`` (a new array; the input is left as is):
+    bandpass_data(flo, fhi) (dvh_sosfiltfilt), then find_noise_idx / impute_noisy_trace for an empty
+    trace and for a noisy trace, then for method 'surface_wave' the per-trace L2 norm
+    (dvh_trace_cleanup).  Host arrays in -> host arrays out (float64 like the reference); device
+    tensors stay on the device.  With return_indices, also the (empty, noisy) trace indices imputed."""
+    if method not in ("surface_wave", "xcorr"):
+        raise AssertionError("method must be 'surface_wave' or 'xcorr'")
+    on_device = isinstance(data, torch.Tensor) and data.is_cuda
+    if on_device:
+        t = data.clone()
+    else:
+        host = np.asarray(data.detach().cpu() if isinstance(data, torch.Tensor) else data, dtype=np.float64)
+        t = torch.from_numpy(np.array(host, copy=True)).to(default_device())
+    if t.dim() != 2:
+        raise ValueError("data must be [n_ch, n_t]")
+    bandpass_inplace(t, dt, flo, fhi)
+    dev = t.device
+    stats = torch.empty(2 * t.shape[0], dtype=torch.float64, device=dev)
+    idx = torch.zeros(2, dtype=torch.int32, device=dev)
+    flags = (1 if impute_empty_traces else 0) | (2 if impute_noise_traces else 0) | (4 if method == "surface_wave" else 0)
+    _lib.call("dvh_trace_cleanup", _lib.ptr(t), 0 if t.dtype == torch.float32 else 1, t.shape[0], t.stride(0),
+              t.shape[1], flags, float(noise_threshold), _lib.ptr(stats), _lib.ptr(idx), _lib.stream_of(dev))
+    out = t if on_device else t.cpu().numpy()
+    if return_indices:
+        return out, tuple(int(i) for i in idx.cpu())
+    return out

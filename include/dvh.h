@@ -129,6 +129,16 @@ int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, 
 int dvh_mute_traj(void* data, int32_t dtype, int32_t n_pass, int64_t pass_stride, int32_t n_ch, int32_t n_t,
                   const int32_t* tab, const double* taper, void* stream);
 
+/* TimeLapseImaging._preprocessing_for_surface_waves after the bandpass (apis/timeLapseImaging.py:
+ * 51-71) on traces x[n_rows][n_t] (row_stride elements): flags 1 = impute the first empty trace
+ * (||x_r|| < noise_threshold), 2 = then the first noisy trace (max x_r > noise_threshold), 4 = then
+ * divide every trace by its L2 norm.  find_noise_idx / impute_noisy_trace (modules/utils.py:316-329)
+ * semantics: np.argmax picks trace 0 when none qualifies; an interior trace becomes the SUM of its
+ * neighbours.  stats: n_rows * 2 doubles of work ({sum x^2, max x} per trace); idx_out (nullable,
+ * 2 ints) receives the imputed trace indices. */
+int dvh_trace_cleanup(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t, int32_t flags,
+                      double noise_threshold, double* stats, int32_t* idx_out, void* stream);
+
 /* SurfaceWaveWindow.mute_along_time (apis/data_classes.py:100-104). */
 int dvh_mute_time(void* data, int32_t dtype, int64_t n_rows, int32_t n_t, const double* taper, void* stream);
 

@@ -96,3 +96,33 @@ def mute_along_traj(data, x_axis, t_axis, veh_state_x, veh_state_t, offset=200, 
 
 def mute_along_time(data, alpha=0.3):
     return np.asarray(data, dtype=np.float64) * tukey(data.shape[-1], alpha)[None, :]
+
+
+def find_noise_idx(data, noise_threshold=5, empty_tr=False):
+    """modules/utils.py:316-321 (np.argmax of the condition: 0 when no trace qualifies)."""
+    if not empty_tr:
+        return np.argmax(np.max(data, axis=1) > noise_threshold)
+    return np.argmax(np.linalg.norm(data, axis=1) < noise_threshold)
+
+
+def impute_noisy_trace(data, noise_idx):
+    """modules/utils.py:323-329 (an interior trace becomes the SUM of its neighbours)."""
+    if noise_idx + 1 == data.shape[0]:
+        data[noise_idx] = data[noise_idx - 1]
+    elif noise_idx == 0:
+        data[noise_idx] = data[noise_idx + 1]
+    else:
+        data[noise_idx] = (data[noise_idx - 1] + data[noise_idx + 1])
+
+
+def surface_wave_prep(data, dt, method="surface_wave", flo=1.2, fhi=30, impute_noise_traces=True, noise_threshold=5,
+                      impute_empty_traces=True):
+    """TimeLapseImaging._preprocessing_for_surface_waves (apis/timeLapseImaging.py:51-71) -> data_for_imaging."""
+    d = bandpass_data(data, dt, flo, fhi)  # returns the filtered copy
+    if impute_empty_traces:
+        impute_noisy_trace(d, find_noise_idx(d, noise_threshold=noise_threshold, empty_tr=True))
+    if impute_noise_traces:
+        impute_noisy_trace(d, find_noise_idx(d, noise_threshold=noise_threshold, empty_tr=False))
+    if method == "surface_wave":
+        d /= np.linalg.norm(d, axis=-1, keepdims=True)
+    return d

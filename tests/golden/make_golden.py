@@ -269,8 +269,42 @@ def gen_ridge(ref):
     return out
 
 
+def gen_prep(ref):
+    """TimeLapseImaging._preprocessing_for_surface_waves (apis/timeLapseImaging.py:51-71) on a
+    continuous record: bandpass, empty / noisy trace imputation (find_noise_idx, impute_noisy_trace,
+    modules/utils.py:316-329), per-trace L2 norm.  Called unbound on a plain object holding the
+    attributes it reads (the constructor's tracking preprocessing is outside the hot path)."""
+    import apis.timeLapseImaging as tli
+    rng = np.random.default_rng(600)
+    n_ch, n_t, dt = 16, 2500, 0.004
+    t = np.arange(n_t) * dt
+    base = np.zeros((n_ch, n_t))
+    for f in (0.5, 3.0, 8.0, 15.0, 40.0):
+        base += 4.0 * np.cos(2 * np.pi * f * t[None, :] + rng.uniform(0, 6.28, (n_ch, 1)))
+    base += 2.0 * rng.standard_normal((n_ch, n_t))
+    cases = {
+        "plain": lambda d: d,                                          # nothing qualifies: trace 0 <- trace 1
+        "dead": lambda d: (d.__setitem__(7, 0.0), d)[1],               # empty trace 7 -> d[6] + d[8]
+        "spike": lambda d: (d.__setitem__((13, slice(1000, 1010)), 400.0), d)[1],  # noisy trace 13
+        "dead_last": lambda d: (d.__setitem__(n_ch - 1, 0.0), d)[1],   # empty last trace -> d[-2]
+        "dead_first_spike": lambda d: (d.__setitem__(0, 0.0), d.__setitem__((5, 200), 900.0), d)[2],
+    }
+    out = dict(dt=np.array(dt))
+    for name, mk in cases.items():
+        d = mk(np.round(base * 2 ** 10) / 2 ** 10)
+        out[name + "_in"] = d.astype(np.float32)  # multiples of 2**-10: exact in float32
+        for method in ("surface_wave", "xcorr"):
+            obj = types.SimpleNamespace(method=method, data=d.copy(), dt=dt, surface_wave_preprecessing_dict=None)
+            tli.TimeLapseImaging._preprocessing_for_surface_waves(obj)
+            out[f"{name}_{method}"] = obj.data_for_imaging
+        bp = d.copy()
+        ref.ut.bandpass_data(bp, dt, 1.2, 30)
+        out[name + "_idx"] = np.array([ref.ut.find_noise_idx(bp, 5, empty_tr=True)])
+    return out
+
+
 GENERATORS = {"vsg_w500": gen_vsg, "vsg_w499": gen_vsg_w499, "vsg_edge": gen_vsg_edge, "disp": gen_disp,
-              "bandpass": gen_bandpass, "ridge": gen_ridge}
+              "bandpass": gen_bandpass, "ridge": gen_ridge, "prep": gen_prep}
 
 
 def main(names=None):

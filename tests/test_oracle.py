@@ -137,3 +137,12 @@ def test_oracle_ridge_and_bootstrap_match_reference():
     rv, f = orid.bootstrap_disp(wins, 3, 4, [25, 50], 700, 500, 900, [80, 130], [2.5, 10], [14, 15], [None, mode1])
     assert np.abs(np.stack(rv[0]) - g["boot_mode0"]).max() < 1e-9
     assert np.abs(np.stack(rv[1]) - g["boot_mode1"]).max() < 1e-9
+
+
+@pytest.mark.parametrize("case", ["plain", "dead", "spike", "dead_last", "dead_first_spike"])
+def test_oracle_surface_wave_prep_matches_reference(case):
+    from oracle import preprocess as op
+    g = gio.load("prep")
+    for m in ("surface_wave", "xcorr"):
+        o = op.surface_wave_prep(g[case + "_in"].astype(np.float64), float(g["dt"]), method=m)
+        assert np.abs(o - g[f"{case}_{m}"]).max() <= 1e-12 * np.abs(g[f"{case}_{m}"]).max()
