@@ -12,6 +12,12 @@ Inputs are resident in HBM before the timed region; the host-side index tables a
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload weights|speeds|synth10k]
 
+synth10k (BASELINE.json configs[2]): 10,240 passes x 1,024 channels x 8,192 samples, single pivot
+at channel 512, all channels in the gather aperture, speed-tercile classes.  The job (335 GB of
+fp32 windows) exceeds HBM, so a pool of 512 passes is resident and a step images the 10,240 passes
+as 20 batches over that pool, each batch with its own 512 per-pass trajectories (index tables);
+window contents repeat across batches, the per-pass work does not.
+
 Prints ONE JSON line (rank 0).  `value` = vehicle-pass windows per second over all ranks.
 """
 from __future__ import annotations
@@ -34,17 +40,21 @@ sys.path.insert(0, ROOT)
 from das_diff_veh_amd.disp import DispPlan, fk_grid, fv_from_fk  # noqa: E402
 from das_diff_veh_amd.distributed import allreduce_stacks, max_over_ranks  # noqa: E402
 from das_diff_veh_amd.plan import VsgParams, VsgPlan, pass_geometry  # noqa: E402
-from das_diff_veh_amd.synth import synth_batch_device  # noqa: E402
+from das_diff_veh_amd.synth import TRACK_DT, synth_batch_device  # noqa: E402
 from das_diff_veh_amd.vsg import StackSchedule, vsg_scales, vsg_stack, window_sumsq  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 WORKLOADS = {
-    # name: (list of (pivot, start_x, end_x, class counts), n_ch, n_t, description)
+    # name: (list of (pivot, start_x, end_x, class counts), n_ch, n_t, description, options)
     "weights": ([(700.0, 500.0, 900.0, (103, 1058, 734)), (680.0, 480.0, 880.0, (103, 1058, 734))], 60, 5500,
-                "configs[1]: 700_weights + 680_weights, heavy/mid/light 103/1058/734 per pivot, 60ch x 5500"),
+                "configs[1]: 700_weights + 680_weights, heavy/mid/light 103/1058/734 per pivot, 60ch x 5500", {}),
     "speeds": ([(700.0, 500.0, 900.0, (330, 1442, 336))], 60, 5500,
-               "configs[0]-shape: 700_speeds, fast/mid/slow 330/1442/336, 60ch x 5500"),
+               "configs[0]-shape: 700_speeds, fast/mid/slow 330/1442/336, 60ch x 5500", {}),
+    "synth10k": ([(4178.0, 0.0, 8400.0, 10240)], 1024, 8192,
+                 "configs[2]: synthetic 10,240 passes x 1024ch x 8192, pivot = channel 512, all channels, "
+                 "speed-tercile classes; 20 batches over a resident pool of 512 passes",
+                 dict(pool=512, x_first=0.37, track_half=4300, gen_chunk=8)),
 }
 
 
@@ -53,25 +63,53 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-class PivotSet:
-    """One window set imaged at one pivot: device windows, index tables, class schedule."""
+class Batch:
+    """One launch's worth of passes: their index tables and class schedule over the resident windows."""
 
-    def __init__(self, pivot, start_x, end_x, counts, n_ch, n_t, seed, device, world, rank):
-        n = int(sum(counts))
+    def __init__(self, plan, sched):
+        self.plan, self.sched = plan, sched
+
+
+class PivotSet:
+    """One window set imaged at one pivot: device windows, index tables, class schedule.
+
+    ``counts`` is either the per-class pass counts (all passes resident) or, with options["pool"],
+    the total number of passes, imaged in batches of `pool` resident windows (speed-tercile classes)."""
+
+    def __init__(self, pivot, start_x, end_x, counts, n_ch, n_t, seed, device, world, rank, opts):
+        pool = opts.get("pool")
+        n = pool or int(sum(counts))
         self.n = n
         t0 = time.time()
-        self.windows, x_axis, t_axis, trk, _ = synth_batch_device(n, n_ch=n_ch, n_t=n_t, pivot=pivot, seed=seed,
-                                                                  device=device)
+        self.windows, x_axis, t_axis, trk, _ = synth_batch_device(
+            n, n_ch=n_ch, n_t=n_t, pivot=pivot, seed=seed, device=device, x_first=opts.get("x_first"),
+            track_half=opts.get("track_half", 350), chunk=opts.get("gen_chunk", 64))
         self.t_gen = time.time() - t0
         t0 = time.time()
         self.prm = VsgParams(pivot=pivot, start_x=start_x, end_x=end_x, wlen=2, norm=False, include_other_side=True)
-        geoms = [pass_geometry(x_axis, t_axis, vx, vt, self.prm) for vx, vt in trk]
-        self.plan = VsgPlan(geoms, self.prm, n_ch, n_t)
         rng = np.random.default_rng(seed + 7)
-        slots = rng.permutation(np.repeat(np.arange(len(counts)), counts))
-        self.slots = slots
+        if pool:
+            n_total = int(counts)
+            n_batch = -(-n_total // pool)
+            xs_trk = trk[0][0]
+            speeds = rng.uniform(15.0, 30.0, n_batch * pool)
+            tcs = t_axis[n_t // 2] + rng.uniform(-1.0, 1.0, n_batch * pool)
+            slots_all = np.searchsorted(np.quantile(speeds, [1 / 3, 2 / 3]), speeds)  # speed terciles
+            counts = np.bincount(slots_all, minlength=3)
+            trks = [(xs_trk, np.round((tc + (xs_trk - pivot) / v) / TRACK_DT) * TRACK_DT) for v, tc in zip(speeds, tcs)]
+            batch_trk = [trks[b * pool:(b + 1) * pool] for b in range(n_batch)]
+            batch_slots = [slots_all[b * pool:(b + 1) * pool] for b in range(n_batch)]
+        else:
+            batch_trk = [trk]
+            batch_slots = [rng.permutation(np.repeat(np.arange(len(counts)), counts))]
+        self.n_total = sum(len(t) for t in batch_trk)
         global_counts = np.asarray(counts) * world  # every rank holds its own full set (weak scaling)
-        self.sched = StackSchedule(slots, len(counts), chunk=8, counts=global_counts)
+        self.batches = []
+        for bt, bs in zip(batch_trk, batch_slots):
+            geoms = [pass_geometry(x_axis, t_axis, vx, vt, self.prm) for vx, vt in bt]
+            plan = VsgPlan(geoms, self.prm, n_ch, n_t)
+            self.batches.append(Batch(plan, StackSchedule(bs, len(counts), chunk=8, counts=global_counts)))
+        self.plan = self.batches[0].plan
         self.t_plan = time.time() - t0
         self.gx, self.gt = geoms[0].gather_x_axis, geoms[0].gather_t_axis
         self.stack = torch.zeros((len(counts), self.plan.R, self.plan.w), dtype=torch.float32, device=device)
@@ -85,27 +123,34 @@ class PivotSet:
         self.disp = DispPlan(e + 1 - s, self.plan.w, 8.16, self.gt[1] - self.gt[0], np.arange(0.8, 25, 0.1),
                              np.arange(200, 1200))
         self.fv = torch.empty((len(counts), self.disp.nV, self.disp.nF), dtype=torch.float32, device=device)
-        self.bytes_stack = self.plan.algorithmic_bytes(out_rows=len(counts) * self.plan.R)
-        self.host = (x_axis, t_axis, trk)
+        self.bytes_stack = [b.plan.algorithmic_bytes(out_rows=len(counts) * self.plan.R) for b in self.batches]
+        self.host = (x_axis, t_axis, batch_trk[0])
 
 
 def build(workload, device, world, rank):
-    sets, n_ch, n_t, desc = WORKLOADS[workload]
+    sets, n_ch, n_t, desc, opts = WORKLOADS[workload]
     out = []
     for i, (pivot, sx, ex, counts) in enumerate(sets):
         out.append(PivotSet(pivot, sx, ex, counts, n_ch, n_t, seed=1000 * rank + 17 * i + 3, device=device,
-                            world=world, rank=rank))
+                            world=world, rank=rank, opts=opts))
     return out, desc
 
 
+def launches(sets):
+    return sum(len(s.batches) for s in sets)
+
+
 def step(sets, world, ev=None):
-    for k, s in enumerate(sets):
-        vsg_scales(s.windows, s.plan, out=s.scales, win_sumsq=s.sumsq)
-        if ev is not None:
-            ev[k][0].record()
-        vsg_stack(s.windows, s.plan, s.sched, scales=s.scales, out=s.stack)
-        if ev is not None:
-            ev[k][1].record()
+    k = 0
+    for s in sets:
+        for j, b in enumerate(s.batches):
+            vsg_scales(s.windows, b.plan, out=s.scales, win_sumsq=s.sumsq)
+            if ev is not None:
+                ev[k][0].record()
+            vsg_stack(s.windows, b.plan, b.sched, scales=s.scales, out=s.stack, accumulate=j > 0)
+            if ev is not None:
+                ev[k][1].record()
+            k += 1
     if world > 1:
         allreduce_stacks([s.stack for s in sets])
     for s in sets:
@@ -133,7 +178,7 @@ def cpu_baseline(sets, budget_s=20.0, workers=None):
     samples = []
     for s in sets:
         x_axis, t_axis, trk = s.host
-        k = min(per_set, s.n)
+        k = min(per_set, s.n, max(4, int(2e9 / (8 * s.windows[0].numel()))))  # host copy <= 2 GB
         host = s.windows[:k].to("cpu", torch.float64).numpy()
         samples.append((host[:16].astype(np.float32), x_axis, t_axis, trk[:16], s.prm))
         t0 = time.time()
@@ -153,7 +198,7 @@ def cpu_baseline(sets, budget_s=20.0, workers=None):
         n_img += 1
     per_window = t_win / n_win
     per_image = t_img / n_img
-    total_windows = sum(s.n for s in sets)
+    total_windows = sum(s.n_total for s in sets)
     total_images = sum(s.stack.shape[0] for s in sets)
     rate1 = total_windows / (per_window * total_windows + per_image * total_images)
     # all cores: single-threaded worker processes (plain python, no torch / GPU state) over a saved
@@ -189,11 +234,13 @@ def cpu_baseline(sets, budget_s=20.0, workers=None):
                 value_1core=rate1)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/<round>_pmc_summary.json, written by tools/pmc.sh: FETCH_SIZE / WRITE_SIZE with the
-    access-width calibration measured by tools/calib/fetch_calib).  (None, None) if absent."""
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), reverse=True):
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this
+    workload (profiles/<round>_pmc_summary[_<workload>].json, written by tools/pmc.sh: FETCH_SIZE /
+    WRITE_SIZE with the access-width calibration measured by tools/calib/fetch_calib).  (None, None)
+    if absent."""
+    sfx = "" if workload == "weights" else "_" + workload
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_summary{sfx}.json")), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -225,13 +272,14 @@ def main():
     sets, desc = build(args.workload, device, world, rank)
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: generated {sum(s.n for s in sets)} windows in {sum(s.t_gen for s in sets):.2f}s, "
-        f"index tables in {sum(s.t_plan for s in sets):.2f}s")
+        f"index tables in {sum(s.t_plan for s in sets):.2f}s; {sum(s.n_total for s in sets)} passes per step, "
+        f"{launches(sets)} stack launches, R = {sets[0].plan.R}")
 
     for _ in range(args.warmup):
         step(sets, world)
     torch.cuda.synchronize()
 
-    ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in sets]
+    ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(launches(sets))]
           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -246,15 +294,15 @@ def main():
     if world > 1:
         elapsed = max_over_ranks(elapsed, device)
 
-    stack_ms = np.array([[ev[k][i][0].elapsed_time(ev[k][i][1]) for i in range(len(sets))]
+    stack_ms = np.array([[ev[k][i][0].elapsed_time(ev[k][i][1]) for i in range(launches(sets))]
                          for k in range(args.steps)])
-    windows_per_step = sum(s.n for s in sets) * world
+    windows_per_step = sum(s.n_total for s in sets) * world
     images_per_step = sum(s.stack.shape[0] for s in sets)
     # roofline of the dominant kernel (vsg_stack): algorithmic bytes per launch / mean launch time
-    bytes_per_launch = float(np.mean([s.bytes_stack for s in sets]))
+    bytes_per_launch = float(np.mean([b for s in sets for b in s.bytes_stack]))
     launch_s = float(stack_ms.mean()) / 1e3
     achieved = bytes_per_launch / launch_s / 1e9
-    traffic, traffic_src = pmc_traffic("vsg_stackf_kernel")
+    traffic, traffic_src = pmc_traffic("vsg_stackf_kernel", args.workload)
     res = {
         "metric": "vehicle-pass windows/sec -> stacked VSG + f-v images/sec; % HBM/MFMA roofline",
         "value": windows_per_step * args.steps / elapsed,

@@ -216,6 +216,42 @@ static int trace_cleanup(T* x, int64_t n_rows, int64_t row_stride, int32_t n_t, 
   return last_launch();
 }
 
+// SurfaceWaveSelector.locate_windows' cut (apis/data_classes.py:208-209, deepcopy of
+// data[x_start:x_start + n_ch, t_start[w]:t_start[w] + n_t]) for all accepted passes at once:
+// out[w][c][t] (contiguous batch, converted to Out).  Reads are guarded against the record's
+// extent; a window outside it sets *status and is left unwritten.
+template <typename In, typename Out>
+__global__ __launch_bounds__(256) void cut_windows_kernel(const In* __restrict__ rec, int64_t n_rows,
+                                                          int64_t row_stride, int64_t rec_n_t,
+                                                          const int64_t* __restrict__ t_start, int64_t x_start,
+                                                          int32_t n_ch, int32_t n_t, Out* __restrict__ out,
+                                                          int32_t* __restrict__ status) {
+  const int64_t w = blockIdx.z;
+  const int c = blockIdx.y;
+  const int64_t ts = t_start[w];
+  if (ts < 0 || ts + n_t > rec_n_t || x_start < 0 || x_start + n_ch > n_rows) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && c == 0 && status) atomicOr(status, 1);
+    return;
+  }
+  const In* src = rec + (x_start + c) * row_stride + ts;
+  Out* dst = out + (w * n_ch + c) * (int64_t)n_t;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n_t; t += gridDim.x * blockDim.x) dst[t] = (Out)src[t];
+}
+
+template <typename In, typename Out>
+static int cut_windows(const void* rec, int64_t n_rows, int64_t row_stride, int64_t rec_n_t, const int64_t* t_start,
+                       int32_t n_win, int64_t x_start, int32_t n_ch, int32_t n_t, void* out, int32_t* status,
+                       hipStream_t s) {
+  const unsigned gx = (unsigned)((n_t + 255) / 256 < 64 ? (n_t + 255) / 256 : 64);
+  for (int32_t w0 = 0; w0 < n_win; w0 += 65535) {  // gridDim.z limit
+    const int32_t nw = n_win - w0 < 65535 ? n_win - w0 : 65535;
+    hipLaunchKernelGGL((cut_windows_kernel<In, Out>), dim3(gx, n_ch, nw), dim3(256), 0, s, (const In*)rec, n_rows,
+                       row_stride, rec_n_t, t_start + w0, x_start, n_ch, n_t,
+                       (Out*)out + (int64_t)w0 * n_ch * n_t, status);
+  }
+  return last_launch();
+}
+
 }  // namespace dvh
 
 using namespace dvh;
@@ -284,4 +320,25 @@ DVH_API int dvh_mute_time(void* data, int32_t dtype, int64_t n_rows, int32_t n_t
   else
     return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
   return last_launch();
+}
+
+DVH_API int dvh_cut_windows(const void* rec, int32_t in_dtype, int64_t n_rows, int64_t row_stride, int64_t rec_n_t,
+                            const int64_t* t_start, int32_t n_win, int64_t x_start, int32_t n_ch, int32_t n_t,
+                            void* out, int32_t out_dtype, int32_t* status, void* stream) {
+  if (!rec || !t_start || !out) return set_error(-2, "null pointer argument");
+  if (n_win < 0 || n_ch < 0 || n_t < 0) return set_error(-2, "invalid sizes");
+  if (n_win == 0 || n_ch == 0 || n_t == 0) return 0;
+  if (n_ch > 65535) return set_error(-4, "too many channels for one launch");
+  if (x_start < 0 || x_start + n_ch > n_rows || n_t > rec_n_t) return set_error(-2, "window outside the record");
+  const hipStream_t s = (hipStream_t)stream;
+  if (in_dtype == 0 && out_dtype == 0)
+    return cut_windows<float, float>(rec, n_rows, row_stride, rec_n_t, t_start, n_win, x_start, n_ch, n_t, out, status, s);
+  if (in_dtype == 1 && out_dtype == 0)
+    return cut_windows<double, float>(rec, n_rows, row_stride, rec_n_t, t_start, n_win, x_start, n_ch, n_t, out, status, s);
+  if (in_dtype == 0 && out_dtype == 1)
+    return cut_windows<float, double>(rec, n_rows, row_stride, rec_n_t, t_start, n_win, x_start, n_ch, n_t, out, status, s);
+  if (in_dtype == 1 && out_dtype == 1)
+    return cut_windows<double, double>(rec, n_rows, row_stride, rec_n_t, t_start, n_win, x_start, n_ch, n_t, out, status,
+                                       s);
+  return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
 }

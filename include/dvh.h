@@ -139,6 +139,15 @@ int dvh_mute_traj(void* data, int32_t dtype, int32_t n_pass, int64_t pass_stride
 int dvh_trace_cleanup(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t, int32_t flags,
                       double noise_threshold, double* stats, int32_t* idx_out, void* stream);
 
+/* SurfaceWaveSelector.locate_windows' cut (apis/data_classes.py:208-216): for every accepted pass w,
+ * out[w][c][t] = rec[x_start + c][t_start[w] + t] (c < n_ch, t < n_t) into a contiguous batch,
+ * converted from in_dtype to out_dtype (0 = float32, 1 = float64).  rec is [n_rows][rec_n_t] with
+ * row_stride elements; t_start (device, n_win int64) is checked on the device: a window outside the
+ * record sets *status (nullable) to 1 and is left unwritten. */
+int dvh_cut_windows(const void* rec, int32_t in_dtype, int64_t n_rows, int64_t row_stride, int64_t rec_n_t,
+                    const int64_t* t_start, int32_t n_win, int64_t x_start, int32_t n_ch, int32_t n_t, void* out,
+                    int32_t out_dtype, int32_t* status, void* stream);
+
 /* SurfaceWaveWindow.mute_along_time (apis/data_classes.py:100-104). */
 int dvh_mute_time(void* data, int32_t dtype, int64_t n_rows, int32_t n_t, const double* taper, void* stream);
 

@@ -29,6 +29,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 from das_diff_veh_amd.synth import synth_pass, DT_W500, DT_W499  # noqa: E402
+from tests.golden_io import select_cases  # noqa: E402
 
 REF = "/root/reference"
 
@@ -303,8 +304,30 @@ def gen_prep(ref):
     return out
 
 
+def gen_select(ref):
+    """SurfaceWaveSelector (apis/data_classes.py:126-223): accepted vehicles, window index ranges and
+    the cut data of every window (float64 record, deep-copied slices)."""
+    out = {}
+    for name, c in select_cases().items():
+        sel = ref.dc.SurfaceWaveSelector(c["rec"], c["dist"], c["t_axis"], c["x0"], c["start_x_tracking"],
+                                         c["veh_states"], c["dist_trk"], c["t_trk"], **c["kw"])
+        rows = []
+        for w in sel.windows:
+            k = next(i for i in range(c["veh_states"].shape[0]) if w.veh_state is c["veh_states"][i]
+                     or np.array_equal(w.veh_state, c["veh_states"][i], equal_nan=True))
+            sx = int(np.flatnonzero(c["dist"] == w.x_axis[0])[0])
+            st = int(np.flatnonzero(c["t_axis"] == w.t_axis[0])[0])
+            rows.append([k, sx, sx + w.data.shape[0], st, st + w.data.shape[1]])
+            assert np.array_equal(w.data, c["rec"][sx:sx + w.data.shape[0], st:st + w.data.shape[1]])
+        out[name + "_windows"] = np.array(rows, dtype=np.int64).reshape(-1, 5)
+        out[name + "_sums"] = np.array([w.data.sum() for w in sel.windows])
+        out[name + "_vx"] = np.concatenate([w.veh_state_x for w in sel.windows]) if sel.windows else np.zeros(0)
+        out[name + "_vt"] = np.concatenate([w.veh_state_t for w in sel.windows]) if sel.windows else np.zeros(0)
+    return out
+
+
 GENERATORS = {"vsg_w500": gen_vsg, "vsg_w499": gen_vsg_w499, "vsg_edge": gen_vsg_edge, "disp": gen_disp,
-              "bandpass": gen_bandpass, "ridge": gen_ridge, "prep": gen_prep}
+              "bandpass": gen_bandpass, "ridge": gen_ridge, "prep": gen_prep, "select": gen_select}
 
 
 def main(names=None):

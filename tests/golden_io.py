@@ -46,3 +46,40 @@ def gather_rel_err(got, ref):
         return 0.0
     scale = np.abs(ref[m]).max()
     return float(np.abs(got[m] - ref[m]).max() / (scale if scale > 0 else 1.0))
+
+
+def select_cases():
+    """Synthetic continuous records + tracked vehicles for SurfaceWaveSelector.locate_windows
+    (apis/data_classes.py:170-223).  veh_states holds tracking-time indices per tracking channel
+    (NaN off the tracked span); x0 - start_x_tracking indexes its column, as the reference does."""
+    rng = np.random.default_rng(700)
+    n_ch, n_t, dt = 48, 6000, 0.004
+    dist = 400.0 + 8.16 * np.arange(n_ch)             # distances_along_fiber of the record
+    dist_trk = 380.0 + 4.08 * np.arange(160)          # tracking grid (finer, offset)
+    t_trk = np.arange(0, n_t * dt, 0.012)             # tracking time axis (3 record samples)
+    rec = np.round(rng.standard_normal((n_ch, n_t)) * 2 ** 8) / 2 ** 8  # exact in float32
+    n_x = 60
+
+    def states(tc):
+        """tracking-time indices of vehicles crossing column 25 at times tc (0.05 s per column)"""
+        vs = np.full((len(tc), n_x), np.nan)
+        for k, t in enumerate(tc):
+            times = t + (np.arange(n_x) - 25) * 0.05
+            ok = (times >= 0) & (times < t_trk[-1])
+            vs[k, ok] = np.round(times[ok] / 0.012)
+            vs[k, :3] = np.nan                         # untracked head of the span
+        return vs
+
+    base = dict(rec=rec, dist=dist, t_axis=np.arange(n_t) * dt, x0=620, start_x_tracking=595, dist_trk=dist_trk,
+                t_trk=t_trk)
+    # crossing times at column x0_idx = 25, in pass order: spacings exercise car-behind (< spacing to the
+    # next), car-ahead (0 <= delta < spacing), a negative delta (not "ahead") and both record boundaries
+    mixed = [0.5, 3.0, 4.0, 4.9, 6.0, 9.9, 10.0, 7.0, 11.7, 14.0, 18.5, 20.2, 23.004]
+    return {
+        "default": dict(base, veh_states=states([3.0, 5.0, 13.5, 22.0, 23.5]), kw={}),  # 2000-sample windows
+        "short": dict(base, veh_states=states(mixed), kw=dict(wlen_sw=2, length_sw=120, spatial_ratio=0.5)),
+        # 499-sample windows: the last crossing sits where t0 + 249 == n_t, so its slice is clipped to 498
+        "odd": dict(base, veh_states=states(mixed), kw=dict(wlen_sw=1.998, length_sw=100, spatial_ratio=0.25,
+                                                              temporal_spacing=0.5)),
+        "spacing": dict(base, veh_states=states(mixed), kw=dict(wlen_sw=1, length_sw=150, temporal_spacing=1.05)),
+    }

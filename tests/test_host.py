@@ -177,3 +177,29 @@ def test_product_does_not_import_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dp, f)).read()
                 assert "import oracle" not in src and "from oracle" not in src, f
+
+
+@pytest.mark.parametrize("case", ["default", "short", "odd", "spacing"])
+def test_pass_table_matches_reference(case):
+    """select.pass_table (host index bookkeeping of locate_windows) vs the reference's windows."""
+    from das_diff_veh_amd.plan import py_slice
+    from das_diff_veh_amd.select import pass_table
+    g = gio.load("select")
+    c = gio.select_cases()[case]
+    t_axis = c["t_axis"]
+    ks, (sx, ex), t0, t1 = pass_table(t_axis, c["dist"], c["x0"], c["start_x_tracking"], c["veh_states"], c["t_trk"],
+                                      t_axis[1] - t_axis[0], **c["kw"])
+    a, n = py_slice(t0, t1, c["rec"].shape[1])
+    got = np.stack([ks, np.full_like(ks, sx), np.full_like(ks, ex), a, a + n], axis=1) if ks.size else \
+        np.zeros((0, 5), np.int64)
+    assert np.array_equal(got, g[case + "_windows"])
+
+
+def test_pass_table_untracked_crossing_raises():
+    """int(nan) in locate_windows raises ValueError; so does the host table."""
+    from das_diff_veh_amd.select import pass_table
+    c = gio.select_cases()["short"]
+    vs = c["veh_states"].copy()
+    vs[2, c["x0"] - c["start_x_tracking"]] = np.nan
+    with pytest.raises(ValueError):
+        pass_table(c["t_axis"], c["dist"], c["x0"], c["start_x_tracking"], vs, c["t_trk"], 0.004, wlen_sw=2)

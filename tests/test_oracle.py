@@ -146,3 +146,27 @@ def test_oracle_surface_wave_prep_matches_reference(case):
     for m in ("surface_wave", "xcorr"):
         o = op.surface_wave_prep(g[case + "_in"].astype(np.float64), float(g["dt"]), method=m)
         assert np.abs(o - g[f"{case}_{m}"]).max() <= 1e-12 * np.abs(g[f"{case}_{m}"]).max()
+
+
+SELECT_CASES = ["default", "short", "odd", "spacing"]
+
+
+@pytest.mark.parametrize("case", SELECT_CASES)
+def test_oracle_window_selection_matches_reference(case):
+    """oracle.select.locate_windows vs SurfaceWaveSelector (apis/data_classes.py:170-223) run in the
+    survey container: accepted passes, slice bounds and the cut data's sums."""
+    from oracle import select as osel
+    g = gio.load("select")
+    c = gio.select_cases()[case]
+    t_axis = c["t_axis"]
+    got = osel.locate_windows(t_axis.size, t_axis, c["dist"], c["x0"], c["start_x_tracking"], c["veh_states"],
+                              c["t_trk"], t_axis[1] - t_axis[0], **c["kw"])
+    ref = g[case + "_windows"]
+    n_t = c["rec"].shape[1]
+    assert [(k, sx, ex, st, min(et, n_t)) for k, sx, ex, st, et in got] == [tuple(r) for r in ref.tolist()]
+    sums = [np.array(c["rec"][sx:ex, st:et]).sum() for _, sx, ex, st, et in got]
+    assert np.array_equal(np.array(sums), g[case + "_sums"])
+    vx = [osel.veh_state_xt(c["veh_states"][k], c["start_x_tracking"], c["dist_trk"], c["t_trk"]) for k, *_ in got]
+    if vx:
+        assert np.array_equal(np.concatenate([v[0] for v in vx]), g[case + "_vx"])
+        assert np.array_equal(np.concatenate([v[1] for v in vx]), g[case + "_vt"])
