@@ -76,7 +76,7 @@ class PivotSet:
     ``counts`` is either the per-class pass counts (all passes resident) or, with options["pool"],
     the total number of passes, imaged in batches of `pool` resident windows (speed-tercile classes)."""
 
-    def __init__(self, pivot, start_x, end_x, counts, n_ch, n_t, seed, device, world, rank, opts):
+    def __init__(self, pivot, start_x, end_x, counts, n_ch, n_t, seed, device, world, rank, opts, chunk=8):
         pool = opts.get("pool")
         n = pool or int(sum(counts))
         self.n = n
@@ -108,7 +108,7 @@ class PivotSet:
         for bt, bs in zip(batch_trk, batch_slots):
             geoms = [pass_geometry(x_axis, t_axis, vx, vt, self.prm) for vx, vt in bt]
             plan = VsgPlan(geoms, self.prm, n_ch, n_t)
-            self.batches.append(Batch(plan, StackSchedule(bs, len(counts), chunk=8, counts=global_counts)))
+            self.batches.append(Batch(plan, StackSchedule(bs, len(counts), chunk=chunk, counts=global_counts)))
         self.plan = self.batches[0].plan
         self.t_plan = time.time() - t0
         self.gx, self.gt = geoms[0].gather_x_axis, geoms[0].gather_t_axis
@@ -127,12 +127,12 @@ class PivotSet:
         self.host = (x_axis, t_axis, batch_trk[0])
 
 
-def build(workload, device, world, rank):
+def build(workload, device, world, rank, chunk=8):
     sets, n_ch, n_t, desc, opts = WORKLOADS[workload]
     out = []
     for i, (pivot, sx, ex, counts) in enumerate(sets):
         out.append(PivotSet(pivot, sx, ex, counts, n_ch, n_t, seed=1000 * rank + 17 * i + 3, device=device,
-                            world=world, rank=rank, opts=opts))
+                            world=world, rank=rank, opts=opts, chunk=chunk))
     return out, desc
 
 
@@ -258,6 +258,7 @@ def main():
     ap.add_argument("--workload", default="weights", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--chunk", type=int, default=8, help="passes per stack task (one wave, one gather row)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -269,7 +270,7 @@ def main():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         dist.init_process_group("nccl", device_id=device)
 
-    sets, desc = build(args.workload, device, world, rank)
+    sets, desc = build(args.workload, device, world, rank, chunk=args.chunk)
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: generated {sum(s.n for s in sets)} windows in {sum(s.t_gen for s in sets):.2f}s, "
         f"index tables in {sum(s.t_plan for s in sets):.2f}s; {sum(s.n_total for s in sets)} passes per step, "
@@ -318,7 +319,7 @@ def main():
         "data": "synthetic (device-generated dispersive moving-source wavefield, per-pass trajectories)",
         "config": {"workload": args.workload, "description": desc, "windows_per_step_per_gpu": windows_per_step // world,
                    "class_images_per_step": images_per_step, "gather_rows": sets[0].plan.R, "w": sets[0].plan.w,
-                   "parallelism": f"dp{world} (passes sharded, all-reduce of class stacks)"},
+                   "parallelism": f"dp{world} (passes sharded, all-reduce of class stacks)", "chunk": args.chunk},
         "images_per_s": images_per_step * args.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,

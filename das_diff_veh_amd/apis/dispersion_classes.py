@@ -11,6 +11,7 @@ from __future__ import annotations
 import copy
 
 import numpy as np
+import torch
 
 from ..modules.utils import Dispersion, disp_plan
 
@@ -78,12 +79,22 @@ class SurfaceWaveDispersion:
 
 
 def batched_surface_wave_dispersion(windows, norm=False, freqs=np.arange(0.8, 25, 0.1), vels=np.arange(200, 1200),
-                                    method="naive", start_x=None, end_x=None, **kw):
+                                    method="naive", start_x=None, end_x=None, mute_offset=None, **kw):
     """(images, avg_image) of ImagesFromWindows.get_images for image_cls=SurfaceWaveDispersion,
-    naive method: one launch per kernel for all windows of a shape."""
+    naive method: one launch per kernel for all windows of a shape.  With ``mute_offset``, every
+    window not yet muted is muted along its trajectory first (mute_along_traj(offset=mute_offset) on
+    a copy, as get_images does): one dvh_mute_traj launch over the device batch, the windows
+    themselves untouched."""
+    from .. import _lib
     from ..device import to_device_f32
     from ..disp import fk_grid, fv_from_fk
+    from ..preprocess import mute_traj_table
     if method != "naive" or kw:
+        if mute_offset is not None:
+            windows = [copy.deepcopy(w) if not w.muted_along_traj else w for w in windows]
+            for w in windows:
+                if not w.muted_along_traj:
+                    w.mute_along_traj(offset=mute_offset)
         images = [SurfaceWaveDispersion(w, freqs=freqs, vels=vels, method=method, norm=norm,
                                         **({} if method != "naive" else dict(start_x=start_x, end_x=end_x)), **kw)
                   for w in windows]
@@ -100,7 +111,23 @@ def batched_surface_wave_dispersion(windows, norm=False, freqs=np.arange(0.8, 25
     acc = None
     per_pass = [None] * n
     for (shape, s, nx, dx, dt), idx in groups.items():
-        data = to_device_f32([windows[i].data for i in idx])[:, s:s + nx, :]
+        data = to_device_f32([windows[i].data for i in idx])
+        mute = [k for k, i in enumerate(idx) if mute_offset is not None and not windows[i].muted_along_traj]
+        if mute:
+            tabs = []
+            for k in mute:
+                w = windows[idx[k]]
+                tab, taper = mute_traj_table(w.x_axis, w.t_axis, w.veh_state_x, w.veh_state_t, offset=mute_offset)
+                tabs.append(tab)
+            sub = data if len(mute) == len(idx) else data[mute].contiguous()
+            dev = sub.device
+            tab_t = torch.from_numpy(np.ascontiguousarray(np.stack(tabs))).to(dev)
+            taper_t = torch.from_numpy(np.ascontiguousarray(taper, dtype=np.float64)).to(dev)
+            _lib.call("dvh_mute_traj", _lib.ptr(sub), 0, len(mute), sub.stride(0), sub.shape[1], sub.shape[2],
+                      _lib.ptr(tab_t), _lib.ptr(taper_t), _lib.stream_of(dev))
+            if sub is not data:
+                data[mute] = sub
+        data = data[:, s:s + nx, :]
         plan = disp_plan(data.shape[1], data.shape[2], dx, dt, freqs, vels)
         FK = fk_grid(data, plan, norm=norm)
         fv = fv_from_fk(FK, plan)

@@ -66,15 +66,11 @@ class DispersionImagesFromWindows(ImagesFromWindows):
         super().__init__(windows, image_cls)
 
     def get_images(self, norm=False, mute_offset=300, mute=True, **imaging_kwargs):
-        """Batched flavour-B path: mute (HIP) + per-pass f-v maps stacked on device."""
+        """Batched flavour-B path: the trajectory mutes of all windows in one launch on a device copy
+        (dvh_mute_traj), then the per-pass f-v maps and their mean on device."""
         from .dispersion_classes import batched_surface_wave_dispersion
-        windows = list(self.windows)
-        if mute:
-            windows = [copy.deepcopy(w) if not w.muted_along_traj else w for w in windows]
-            for w in windows:
-                if not w.muted_along_traj:
-                    w.mute_along_traj(offset=mute_offset)
-        self.images, self.avg_image = batched_surface_wave_dispersion(windows, norm=norm, **imaging_kwargs)
+        self.images, self.avg_image = batched_surface_wave_dispersion(
+            list(self.windows), norm=norm, mute_offset=mute_offset if mute else None, **imaging_kwargs)
 
 
 class VirtualShotGathersFromWindows(ImagesFromWindows):

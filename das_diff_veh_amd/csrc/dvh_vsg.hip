@@ -36,7 +36,7 @@
 
 namespace dvh {
 
-constexpr int kBlock = 256;  // sumsq kernel
+constexpr int kBlock = 512;  // sumsq kernel
 // waves per SIMD the kernels are compiled for: one 7-wave Eng500 block (145 KB LDS) per CU;
 // the Stockham engines are register-limited to 3
 template <class E> struct Occ { static constexpr int v = 3; };
@@ -464,27 +464,55 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
 }
 
 // Sum of squares of each pass window (np.linalg.norm(window.data) ** 2), for norm=norm_amp=False.
+// One block per pass; wave k takes rows k, k + 8, ...; 16-byte loads, 4 in flight per lane, fp64
+// accumulation in a fixed order (deterministic run to run).
+constexpr int kSumWaves = kBlock / 64;
 __global__ __launch_bounds__(kBlock) void window_sumsq_kernel(const float* __restrict__ win, int64_t pass_stride,
                                                                int64_t ch_stride, int32_t n_ch, int32_t n_t,
                                                                double* __restrict__ out) {
-  __shared__ double part[kBlock / 64];
+  __shared__ double part[kSumWaves];
   const int p = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* base = win + (int64_t)p * pass_stride;
-  double s = 0.0;
-  for (int c = 0; c < n_ch; ++c) {
+  const bool vec = (n_t % 4 == 0) && (ch_stride % 4 == 0) && (pass_stride % 4 == 0) &&
+                   (reinterpret_cast<uintptr_t>(win) % 16 == 0);
+  double s0 = 0.0, s1 = 0.0;
+  for (int c = wave; c < n_ch; c += kSumWaves) {
     const float* row = base + (int64_t)c * ch_stride;
-    for (int t = threadIdx.x; t < n_t; t += blockDim.x) {
-      const double v = row[t];
-      s += v * v;
+    if (vec) {
+      const float4* r4 = reinterpret_cast<const float4*>(row);
+      const int n4 = n_t / 4;
+      int t = lane;
+      for (; t + 192 < n4; t += 256) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = r4[t + 64 * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s0 += (double)v[u].x * v[u].x + (double)v[u].y * v[u].y;
+          s1 += (double)v[u].z * v[u].z + (double)v[u].w * v[u].w;
+        }
+      }
+      for (; t < n4; t += 64) {
+        const float4 v = r4[t];
+        s0 += (double)v.x * v.x + (double)v.y * v.y;
+        s1 += (double)v.z * v.z + (double)v.w * v.w;
+      }
+    } else {
+      for (int t = lane; t < n_t; t += 64) {
+        const double v = row[t];
+        s0 += v * v;
+      }
     }
   }
+  double s = s0 + s1;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  if (lane == 0) part[wave] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
-    for (int k = 0; k < kBlock / 64; ++k) t += part[k];
+    for (int k = 0; k < kSumWaves; ++k) t += part[k];
     out[p] = t;
   }
 }

@@ -22,8 +22,23 @@ namespace dvh {
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+#ifndef DVH_PK_CMUL
+#define DVH_PK_CMUL 1
+#endif
+typedef float pk2 __attribute__((ext_vector_type(2)));
+// a * b.  Packed form: two VALU ops (v_pk_mul_f32 of (a.x b.x, a.x b.y), then v_pk_fma_f32 adding
+// (-a.y b.y, a.y b.x) through operand selects / negation), where the compiler's own packed
+// lowering spends three packed products plus two moves per complex multiply.
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+#if DVH_PK_CMUL
+  const pk2 av = {a.x, a.y}, bv = {b.x, b.y};
+  pk2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(av), "v"(bv));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(av), "v"(bv), "v"(t));
+  return make_float2(r.x, r.y);
+#else
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+#endif
 }
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 // -i * a and +i * a

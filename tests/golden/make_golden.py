@@ -326,8 +326,31 @@ def gen_select(ref):
     return out
 
 
+def gen_tli(ref):
+    """TimeLapseImaging's imaging half end to end (apis/timeLapseImaging.py:50-71, 166-201), flavour B:
+    preprocessing of the continuous record, SurfaceWaveSelector, DispersionImagesFromWindows (trajectory
+    mute, naive dispersion per window, mean).  Called unbound on a plain object holding the tracking
+    results (the tracker itself is outside the hot path)."""
+    import apis.timeLapseImaging as tli
+    c = select_cases()["short"]
+    x_axis = 449.0 + np.arange(c["rec"].shape[0])
+    obj = types.SimpleNamespace(method="surface_wave", data=c["rec"].copy(), dt=c["t_axis"][1] - c["t_axis"][0],
+                                t_axis=c["t_axis"], x_axis=x_axis, distances_along_fiber=(x_axis - 400) * 8.16,
+                                surface_wave_preprecessing_dict=None, start_x=c["start_x_tracking"],
+                                veh_states=c["veh_states"], dist_along_fiber_tracking=c["dist_trk"],
+                                t_axis_tracking=c["t_trk"])
+    T = tli.TimeLapseImaging
+    T._preprocessing_for_surface_waves(obj)
+    T.select_surface_wave_windows(obj, c["x0"], **c["kw"])
+    T.get_images(obj, mute_offset=300, start_x=560, end_x=680)
+    return dict(x_axis=x_axis, n_windows=np.array(len(obj.sw_selector.windows)),
+                fv_avg=obj.images.avg_image.disp.fv_map, fv_first=obj.images.images[0].disp.fv_map,
+                qs_first=obj.qs_selector.windows[0].data)
+
+
 GENERATORS = {"vsg_w500": gen_vsg, "vsg_w499": gen_vsg_w499, "vsg_edge": gen_vsg_edge, "disp": gen_disp,
-              "bandpass": gen_bandpass, "ridge": gen_ridge, "prep": gen_prep, "select": gen_select}
+              "bandpass": gen_bandpass, "ridge": gen_ridge, "prep": gen_prep, "select": gen_select,
+              "tli": gen_tli}
 
 
 def main(names=None):
