@@ -45,13 +45,13 @@ def _compile(src, verbose=False):
     return obj
 
 
-def build(verbose=False, jobs=None, out=None, defines=()):
-    """Build libdvh.so (or, with out/defines, a variant library for A/B timing)."""
+def build(verbose=False, jobs=None, out=None, defines=(), flags=()):
+    """Build libdvh.so (or, with out/defines/flags, a variant library for A/B timing)."""
     global LIB, OBJ_DIR, CFLAGS
     if out is not None:
         saved = LIB, OBJ_DIR, CFLAGS
         LIB, OBJ_DIR = out, out + ".obj"
-        CFLAGS = CFLAGS + [f"-D{d}" for d in defines]
+        CFLAGS = CFLAGS + [f"-D{d}" for d in defines] + list(flags)
         try:
             return build(verbose, jobs)
         finally:

@@ -11,8 +11,20 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#ifndef DVH_NO_READ2
+#define DVH_NO_READ2 0
+#endif
+// One LDS complex read.  With DVH_NO_READ2 the index is made opaque so that the compiler cannot
+// pair reads into ds_read2_b64 (8 LDS cycles on gfx950 against 2 + 2 for two ds_read_b64).
+__device__ __forceinline__ float2 lds_ld(const float2* p, int idx) {
+#if DVH_NO_READ2
+  asm volatile("" : "+v"(idx));
+#endif
+  return p[idx];
+}
+
 #ifndef DVH_STAGE_UNROLL
-#define DVH_STAGE_UNROLL 0
+#define DVH_STAGE_UNROLL 1
 #endif
 #ifndef DVH_TW_RECUR
 #define DVH_TW_RECUR 1
@@ -23,19 +35,26 @@ namespace dvh {
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 #ifndef DVH_PK_CMUL
-#define DVH_PK_CMUL 1
+#define DVH_PK_CMUL 0
 #endif
 typedef float pk2 __attribute__((ext_vector_type(2)));
-// a * b.  Packed form: two VALU ops (v_pk_mul_f32 of (a.x b.x, a.x b.y), then v_pk_fma_f32 adding
-// (-a.y b.y, a.y b.x) through operand selects / negation), where the compiler's own packed
-// lowering spends three packed products plus two moves per complex multiply.
+// a * b.  Default (0): plain C.  1: two packed ops (v_pk_mul_f32, then v_pk_fma_f32 with operand
+// selects / negation); 2: four scalar ops in asm.  Measured on the N = 500 stack kernel: packed
+// forms are no faster than scalar FMAs on gfx950 (1 was 2-3 % slower), so the default stays C.
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-#if DVH_PK_CMUL
+#if DVH_PK_CMUL == 1
   const pk2 av = {a.x, a.y}, bv = {b.x, b.y};
   pk2 t, r;
   asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(av), "v"(bv));
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(av), "v"(bv), "v"(t));
   return make_float2(r.x, r.y);
+#elif DVH_PK_CMUL == 2
+  float re, im;  // four scalar VALU ops (kept out of packed form)
+  asm("v_mul_f32 %0, %1, %2" : "=v"(re) : "v"(a.y), "v"(b.y));
+  asm("v_fma_f32 %0, %1, %2, -%3" : "=v"(re) : "v"(a.x), "v"(b.x), "v"(re));
+  asm("v_mul_f32 %0, %1, %2" : "=v"(im) : "v"(a.y), "v"(b.x));
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(im) : "v"(a.x), "v"(b.y), "v"(im));
+  return make_float2(re, im);
 #else
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 #endif
@@ -111,18 +130,13 @@ __device__ __forceinline__ void stockham_stage(const float2* __restrict__ in, fl
   constexpr int NB = N / R;
   constexpr int TWS = N / (Ls * R);
   static_assert(N % (Ls * R) == 0, "plan does not divide N");
-#if DVH_STAGE_UNROLL
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
-  for (int i0 = 0; i0 < NB; i0 += 64) {
+  auto round = [&](int i0) {
     const int i = i0 + lane;
     if (NB % 64 == 0 || i < NB) {
       const int k = i % Ls;
       float2 a[R];
 #pragma unroll
-      for (int t = 0; t < R; ++t) a[t] = in[i + t * NB];
+      for (int t = 0; t < R; ++t) a[t] = lds_ld(in, i + t * NB);
       if (Ls > 1) {
 #if DVH_TW_RECUR
         // one table read per butterfly, powers by recurrence (LDS reads are the scarcer resource)
@@ -143,6 +157,16 @@ __device__ __forceinline__ void stockham_stage(const float2* __restrict__ in, fl
 #pragma unroll
       for (int q = 0; q < R; ++q) out[base + q * Ls] = a[q];
     }
+  };
+  // Short radix <= 5 stages (<= 2 rounds of 64 butterflies) are unrolled so that the second round's LDS reads
+  // overlap the first round's arithmetic (measured -8 % on the N = 500 stack kernel); long ones stay
+  // rolled (code size, registers).
+  if constexpr (DVH_STAGE_UNROLL && NB <= 128 && R <= 5) {
+#pragma unroll
+    for (int i0 = 0; i0 < NB; i0 += 64) round(i0);
+  } else {
+#pragma unroll 1
+    for (int i0 = 0; i0 < NB; i0 += 64) round(i0);
   }
 }
 

@@ -537,6 +537,12 @@ struct Eng500 {
 //     five bins in registers -- no LDS write of the spectrum and no partner reads.
 // Half-spectrum slots per lane l: j < 3 -> f = l + 100 j (l <= 50); j = 3, 4 -> f = 100 - l + 100 (j - 3)
 // (1 <= l <= 49): each of the 251 bins f <= 250 exactly once.
+#ifndef DVH_DIAG_NOLOAD
+#define DVH_DIAG_NOLOAD 0
+#endif
+#ifndef DVH_DIAG_SKIP
+#define DVH_DIAG_SKIP 0
+#endif
 struct EngF500 {
   static constexpr int N = 500;
   static constexpr int NFFT = 500;
@@ -572,7 +578,11 @@ struct EngF500 {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int n = a + i + 125 * u;
+#if DVH_DIAG_NOLOAD  // timing diagnostic only (wrong results): no global reads
+        z[4 * r + u] = (i < 125) ? make_float2(1.f + 1e-3f * (float)(n & 255), 1.f - 1e-3f * (float)u) : make_float2(0.f, 0.f);
+#else
         z[4 * r + u] = (i < 125) ? make_float2(t.piv[n], t.rcv[n]) : make_float2(0.f, 0.f);
+#endif
       }
     }
   }
@@ -600,9 +610,13 @@ struct EngF500 {
   template <class F>
   __device__ __forceinline__ void finish_with(F&& acc) const {
     wave_sync();
+#if DVH_DIAG_SKIP != 1  // timing diagnostics only (wrong results): 1 omits stage 2, 2 omits stage 3
     stockham_stage<N, 4, 5>(bufB, bufA, tw, lane);
     wave_sync();
+#endif
+#if DVH_DIAG_SKIP != 2
     stockham_stage<N, 20, 5>(bufA, bufB, tw, lane);
+#endif
     wave_sync();
     if (lane <= 50) {
       float2 XA[5], XB[5];
@@ -629,7 +643,7 @@ struct EngF500 {
   // radix-5 butterfly k of the last stage (span 100): X[k + 100 q], q < 5
   __device__ __forceinline__ void last_bfly_from(const float2* src, int k, float2 (&x)[5]) const {
 #pragma unroll
-    for (int t = 0; t < 5; ++t) x[t] = src[k + 100 * t];
+    for (int t = 0; t < 5; ++t) x[t] = lds_ld(src, k + 100 * t);
     const float2 w1 = tw[k];
     float2 wt = w1;
 #pragma unroll
