@@ -41,6 +41,7 @@ constexpr int kBlock = 512;  // sumsq kernel
 // the Stockham engines are register-limited to 3
 template <class E> struct Occ { static constexpr int v = 3; };
 template <> struct Occ<EngF500> { static constexpr int v = 4; };
+template <> struct Occ<EngP500> { static constexpr int v = 4; };
 template <> struct Occ<Eng500> { static constexpr int v = 2; };
 #ifndef DVH_STACKF_OCC
 #define DVH_STACKF_OCC 0
@@ -558,9 +559,11 @@ static bool get_kernels(int w, VsgKernels* k, int* n_out) {
   *n_out = n;
   switch (n) {
     case 250: *k = vsg_kernels<EngStockham<250, false>, true>(); return true;
-    case 500:  // 0: fused-stage Stockham (default), 1: 20 x 25 register engine, 2: plain Stockham
+    case 500:  // 0: fused-stage Stockham (default), 1: 20 x 25 register engine, 2: plain Stockham,
+               // 3: paired 20 x 5 x 5 in-place engine
       *k = DVH_VSG500 == 1   ? vsg_kernels<Eng500, true>()
            : DVH_VSG500 == 2 ? vsg_kernels<EngStockham<500, false>, true>()
+           : DVH_VSG500 == 3 ? vsg_kernels<EngP500, true>()
                              : vsg_kernels<EngF500, true>();
       return true;
     case 1000: *k = vsg_kernels<EngStockham<1000, false>, true>(); return true;

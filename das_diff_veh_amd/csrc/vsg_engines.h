@@ -537,6 +537,9 @@ struct Eng500 {
 //     five bins in registers -- no LDS write of the spectrum and no partner reads.
 // Half-spectrum slots per lane l: j < 3 -> f = l + 100 j (l <= 50); j = 3, 4 -> f = 100 - l + 100 (j - 3)
 // (1 <= l <= 49): each of the 251 bins f <= 250 exactly once.
+#ifndef DVH_XB_ALWAYS
+#define DVH_XB_ALWAYS 0
+#endif
 #ifndef DVH_DIAG_NOLOAD
 #define DVH_DIAG_NOLOAD 0
 #endif
@@ -622,7 +625,11 @@ struct EngF500 {
       float2 XA[5], XB[5];
       last_bfly_from(bufB, lane, XA);
       const bool pair = lane >= 1 && lane <= 49;
+#if DVH_XB_ALWAYS  // lanes 0 and 50 recompute their own butterfly: no branch between the two
+      last_bfly_from(bufB, pair ? 100 - lane : lane, XB);
+#else
       if (pair) last_bfly_from(bufB, 100 - lane, XB);
+#endif
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         // partner X[N - f] of f = l + 100 j is X[(100 - l) + 100 (4 - j)]
@@ -644,6 +651,7 @@ struct EngF500 {
   __device__ __forceinline__ void last_bfly_from(const float2* src, int k, float2 (&x)[5]) const {
 #pragma unroll
     for (int t = 0; t < 5; ++t) x[t] = lds_ld(src, k + 100 * t);
+#if DVH_TW_RECUR
     const float2 w1 = tw[k];
     float2 wt = w1;
 #pragma unroll
@@ -651,6 +659,10 @@ struct EngF500 {
       x[t] = cmul(x[t], wt);
       if (t < 4) wt = cmul(wt, w1);
     }
+#else
+#pragma unroll
+    for (int t = 1; t < 5; ++t) x[t] = cmul(x[t], tw[t * k]);
+#endif
     Dft<5>::run(x);
   }
 
@@ -705,6 +717,231 @@ struct EngF500 {
   __device__ float2 c(const float2* Y, int k, int) const {
     const float2 v = Y[k];
     return make_float2(v.x, -v.y);
+  }
+};
+
+
+// EngP500: N = w = 500 with TWO sub-windows of the row task per transform pass (lanes 0-31 carry
+// transform 0, lanes 32-63 transform 1) and one LDS round trip fewer than EngF500:
+//   500 = 20 x 5 x 5, n = n2 + 25 n1, f = k1 + 20 j1 + 100 j2
+//   stage 1  lane n2 < 25 of its half: the 20 samples x[n2 + 25 n1] straight from global memory,
+//            a radix-20 (4 x 5, compile-time twiddles) in registers, x W500^(n2 k1) by recurrence,
+//            20 LDS writes                                      (25 of 32 lanes busy)
+//   stage 2  200 radix-5 butterflies (k1, m2) over m1, x W25^(m2 j1), written back IN PLACE
+//            (the butterfly's five slots), 4 rounds
+//   stage 3  the last radix-5 (k1, j1) over m2: bins b + 100 j2 of butterfly b = k1 + 20 j1 --
+//            EngF500's last-stage layout, so the half-spectrum slots, partner pairing and the
+//            cross-spectrum accumulation are EngF500's (lane l <= 50: butterflies l and 100 - l)
+// Per transform the LDS traffic is 500 writes + 500 reads fewer than EngF500's three round trips;
+// each transform owns one in-place buffer of 27 x 20 slots (pos = 27 k1 + n2: conflict-free stage-1
+// stores, <= 1.6-way reads).
+#ifndef DVH_P500_S2UNROLL
+#define DVH_P500_S2UNROLL 0
+#endif
+#ifndef DVH_P500_NOPF
+#define DVH_P500_NOPF 0
+#endif
+#ifndef DVH_P500_PAD
+#define DVH_P500_PAD 27
+#endif
+struct EngP500 : EngF500 {
+  static constexpr int S = DVH_P500_PAD;
+  static constexpr int kBuf = 19 * S + 25;                      // slots per transform buffer
+  static constexpr size_t kWaveBytes = sizeof(float2) * 2 * kBuf;  // two in-place buffers
+  float2* buf1;
+
+  __device__ EngP500(char* lds, int wave, int lane_) : EngF500(lds, wave, lane_) {
+    bufA = reinterpret_cast<float2*>(lds + kBlockBytes + (size_t)wave * kWaveBytes);
+    bufB = bufA + kBuf;
+    buf1 = bufB;
+  }
+  static __device__ __forceinline__ int pos(int n2, int k1) { return S * k1 + n2; }
+
+  // W20^m, m <= 12 (the q r products of the radix-20): (cos, -sin)(2 pi m / 20)
+  static __device__ __forceinline__ float2 w20(int m) {
+    constexpr float c[13] = {1.f, 0.951056516f, 0.809016994f, 0.587785252f, 0.309016994f, 0.f, -0.309016994f,
+                             -0.587785252f, -0.809016994f, -0.951056516f, -1.f, -0.951056516f, -0.809016994f};
+    constexpr float n[13] = {0.f, -0.309016994f, -0.587785252f, -0.809016994f, -0.951056516f, -1.f, -0.951056516f,
+                             -0.809016994f, -0.587785252f, -0.309016994f, 0.f, 0.309016994f, 0.587785252f};
+    return make_float2(c[m], n[m]);
+  }
+
+  // the pair's samples: lane half h -> sub-window starting at a_h, n2 = lane & 31 < 25
+  __device__ __forceinline__ void load2(const RowTask& t, int a0, int a1, bool two, float (&zp)[20],
+                                        float (&zr)[20]) const {
+    const int h = lane >> 5, n2 = lane & 31;
+    const bool ok = n2 < 25 && (h == 0 || two);
+    const int a = (h ? a1 : a0) + n2;
+#pragma unroll
+    for (int n1 = 0; n1 < 20; ++n1) {
+      zp[n1] = ok ? t.piv[a + 25 * n1] : 0.f;
+      zr[n1] = ok ? t.rcv[a + 25 * n1] : 0.f;
+    }
+  }
+
+  __device__ __forceinline__ void stage1(const float (&zp)[20], const float (&zr)[20], bool two) const {
+    const int h = lane >> 5, n2 = lane & 31;
+    if (n2 < 25 && (h == 0 || two)) {
+      float2 A[20];  // A[r + 4 s]
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        float2 a[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) a[p] = make_float2(zp[5 * p + q], zr[5 * p + q]);
+        Dft<4>::run(a);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = q * r;
+          float2 v = a[r];
+          if (m == 5) v = mul_mi(v);
+          else if (m == 10) v = make_float2(-v.x, -v.y);
+          else if (m != 0) v = cmul(v, w20(m));
+          A[r + 4 * q] = v;  // D[q][r], parked in A until the radix-5 pass
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // in place: A[r + 4 s] <- radix-5 over q of A[r + 4 q]
+        float2 e[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) e[q] = A[r + 4 * q];
+        Dft<5>::run(e);
+#pragma unroll
+        for (int s2 = 0; s2 < 5; ++s2) A[r + 4 * s2] = e[s2];
+      }
+      float2* buf = h ? buf1 : bufA;
+      const float2 w1 = tw[n2];
+      float2 w = w1;
+      buf[pos(n2, 0)] = A[0];
+#pragma unroll
+      for (int k1 = 1; k1 < 20; ++k1) {
+        buf[pos(n2, k1)] = cmul(A[k1], w);
+        if (k1 < 19) w = cmul(w, w1);
+      }
+    }
+  }
+
+  // stage 2 over both transforms: task T = 64 r + lane < 100 (1 + two): (k1, m2) = (u % 20, u / 20)
+  __device__ __forceinline__ void stage2(bool two) const {
+    const int nt = two ? 200 : 100;
+    auto round = [&](int r) {
+      const int T = 64 * r + lane;
+      if (T < nt) {
+        const int f = T >= 100, u = T - 100 * f;
+        const int k1 = u % 20, m2 = u / 20;
+        float2* buf = f ? buf1 : bufA;
+        float2 x[5];
+#pragma unroll
+        for (int m1 = 0; m1 < 5; ++m1) x[m1] = buf[pos(m2 + 5 * m1, k1)];
+        Dft<5>::run(x);
+        const float2 w1 = tw[20 * m2];  // W25^m2
+        float2 w = w1;
+#pragma unroll
+        for (int j1 = 1; j1 < 5; ++j1) {
+          x[j1] = cmul(x[j1], w);
+          if (j1 < 4) w = cmul(w, w1);
+        }
+#pragma unroll
+        for (int j1 = 0; j1 < 5; ++j1) buf[pos(m2 + 5 * j1, k1)] = x[j1];
+      }
+    };
+#if DVH_P500_S2UNROLL
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+    for (int r = 0; r < 4; ++r) round(r);
+  }
+
+  // last radix-5 of butterfly b (k1 = b % 20, j1 = b / 20): X[b + 100 j2]
+  __device__ __forceinline__ void last_p(const float2* buf, int b, float2 (&x)[5]) const {
+    const int k1 = b % 20, j1 = b / 20;
+#pragma unroll
+    for (int m2 = 0; m2 < 5; ++m2) x[m2] = buf[pos(5 * j1 + m2, k1)];
+    Dft<5>::run(x);
+  }
+
+  // stage 3 of transform buf into the half-spectrum slots (EngF500::finish_with's pairing)
+  template <class F>
+  __device__ __forceinline__ void finish_p(const float2* buf, F&& acc) const {
+    if (lane <= 50) {
+      float2 XA[5], XB[5];
+      last_p(buf, lane, XA);
+      const bool pair = lane >= 1 && lane <= 49;
+      last_p(buf, pair ? 100 - lane : lane, XB);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const float2 p0 = XA[(5 - j) % 5], p50 = XA[4 - j], pb = XB[4 - j];
+        float2 pa;
+        pa.x = lane == 0 ? p0.x : (lane == 50 ? p50.x : pb.x);
+        pa.y = lane == 0 ? p0.y : (lane == 50 ? p50.y : pb.y);
+        acc(j, XA[j], pa);
+      }
+      if (pair) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) acc(3 + q, XB[q], XA[4 - q]);
+      }
+    }
+  }
+
+  __device__ void spectra(const RowTask& t, const RowTask&, bool, int, int hop, float2 (&Cf)[NH], float2 (&Co)[NH]) {
+    const int nq = t.nwin_f + t.nwin_o;
+    float zp[20], zr[20];
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      Cf[j] = make_float2(0.f, 0.f);
+      Co[j] = make_float2(0.f, 0.f);
+    }
+    live_f = live_o = false;
+    auto start = [&](int q) { return q < t.nwin_f ? t.a_f + q * hop : t.a_o + (q - t.nwin_f) * hop; };
+    if (nq > 0) load2(t, start(0), nq > 1 ? start(1) : 0, nq > 1, zp, zr);
+    for (int q = 0; q < nq; q += 2) {
+      const bool two = q + 1 < nq;
+      uint32_t bp = 0, br = 0;
+#pragma unroll
+      for (int j = 0; j < 20; ++j) {
+        bp |= nzbits(zp[j]);
+        br |= nzbits(zr[j]);
+      }
+      const uint64_t mp = __ballot(bp != 0), mr = __ballot(br != 0);
+      const bool live0 = (mp & 0xffffffffull) && (mr & 0xffffffffull);
+      const bool live1 = two && (mp >> 32) && (mr >> 32);
+      if (live0 || live1) stage1(zp, zr, two);
+#if !DVH_P500_NOPF
+      if (q + 2 < nq) load2(t, start(q + 2), q + 3 < nq ? start(q + 3) : 0, q + 3 < nq, zp, zr);
+#endif
+      if (!(live0 || live1)) continue;  // exactly zero in the reference
+      wave_sync();
+      stage2(two);
+      wave_sync();
+      if (live0) {
+        if (q < t.nwin_f) {
+          live_f = true;
+          finish_p(bufA, [&](int j, float2 a, float2 b) { accumulate_cross(a, b, Cf[j]); });
+        } else {
+          live_o = true;
+          finish_p(bufA, [&](int j, float2 a, float2 b) { accumulate_cross(a, b, Co[j]); });
+        }
+      }
+      if (live1) {
+        if (q + 1 < t.nwin_f) {
+          live_f = true;
+          finish_p(buf1, [&](int j, float2 a, float2 b) { accumulate_cross(a, b, Cf[j]); });
+        } else {
+          live_o = true;
+          finish_p(buf1, [&](int j, float2 a, float2 b) { accumulate_cross(a, b, Co[j]); });
+        }
+      }
+      wave_sync();
+#if DVH_P500_NOPF
+      if (q + 2 < nq) load2(t, start(q + 2), q + 3 < nq ? start(q + 3) : 0, q + 3 < nq, zp, zr);
+#endif
+    }
+  }
+
+  __device__ const float2* correlate(const RowTask& t, const RowTask& nt, bool has_next, int w, int hop) {
+    float2 Cf[NH], Co[NH];
+    spectra(t, nt, has_next, w, hop, Cf, Co);
+    return inverse(Cf, Co);
   }
 };
 
