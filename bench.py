@@ -94,7 +94,10 @@ class PivotSet:
             xs_trk = trk[0][0]
             speeds = rng.uniform(15.0, 30.0, n_batch * pool)
             tcs = t_axis[n_t // 2] + rng.uniform(-1.0, 1.0, n_batch * pool)
-            slots_all = np.searchsorted(np.quantile(speeds, [1 / 3, 2 / 3]), speeds)  # speed terciles
+            # speed terciles by rank (exact, equal-as-possible counts: every rank has the same class
+            # sizes, so the global counts are world x the local ones)
+            slots_all = np.empty(speeds.size, dtype=np.int64)
+            slots_all[np.argsort(speeds, kind="stable")] = np.arange(speeds.size) * 3 // speeds.size
             counts = np.bincount(slots_all, minlength=3)
             trks = [(xs_trk, np.round((tc + (xs_trk - pivot) / v) / TRACK_DT) * TRACK_DT) for v, tc in zip(speeds, tcs)]
             batch_trk = [trks[b * pool:(b + 1) * pool] for b in range(n_batch)]
