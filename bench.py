@@ -10,13 +10,18 @@ all-reduce of the partial class stacks], then the f-v image of every class stack
 (compute_disp_image(end_x=0, start_x=-200): 1,000 velocities x 242 frequencies).
 Inputs are resident in HBM before the timed region; the host-side index tables are built once.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload weights|speeds|synth10k]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload weights|speeds|synth10k|sliding]
 
 synth10k (BASELINE.json configs[2]): 10,240 passes x 1,024 channels x 8,192 samples, single pivot
 at channel 512, all channels in the gather aperture, speed-tercile classes.  The job (335 GB of
 fp32 windows) exceeds HBM, so a pool of 512 passes is resident and a step images the 10,240 passes
 as 20 batches over that pool, each batch with its own 512 per-pass trajectories (index tables);
 window contents repeat across batches, the per-pass work does not.
+
+sliding (BASELINE.json configs[3]): 4,096-channel x 8,192-sample windows imaged at sliding pivots
+(every 8 channels, +-200 m) -- one unit per (pass, pivot crossed inside the window), slots = speed
+class x pivot, one f-v image per slot (SlidingSet).  12,544 passes per GPU per step (100k over 8
+GPUs), 49 batches over a resident pool of 256 windows (34 GB).
 
 Prints ONE JSON line (rank 0).  `value` = vehicle-pass windows per second over all ranks.
 """
@@ -51,6 +56,12 @@ WORKLOADS = {
                 "configs[1]: 700_weights + 680_weights, heavy/mid/light 103/1058/734 per pivot, 60ch x 5500", {}),
     "speeds": ([(700.0, 500.0, 900.0, (330, 1442, 336))], 60, 5500,
                "configs[0]-shape: 700_speeds, fast/mid/slow 330/1442/336, 60ch x 5500", {}),
+    "sliding": ([(None, None, None, 12544)], 4096, 8192,
+                "configs[3]: synthetic passes x 4096ch x 8192, sliding pivots every 8 channels (+-200 m, 49 rows), "
+                "each pass imaged at every pivot it crosses inside its window; 12,544 passes per GPU (100k over 8) "
+                "as 49 batches over a resident pool of 256 passes; speed classes x pivots stacked, f-v image per "
+                "(class, pivot)",
+                dict(sliding=True, pool=256, pivot_every=8, half_aperture=200.0, gen_chunk=2)),
     "synth10k": ([(4178.0, 0.0, 8400.0, 10240)], 1024, 8192,
                  "configs[2]: synthetic 10,240 passes x 1024ch x 8192, pivot = channel 512, all channels, "
                  "speed-tercile classes; 20 batches over a resident pool of 512 passes",
@@ -64,10 +75,12 @@ def log(*a):
 
 
 class Batch:
-    """One launch's worth of passes: their index tables and class schedule over the resident windows."""
+    """One launch's worth of passes: their index tables and class schedule over the resident windows
+    (``win`` / ``sumsq``: the launch view of the windows and its per-pass ||window||_F^2)."""
 
-    def __init__(self, plan, sched):
+    def __init__(self, plan, sched, win=None, sumsq=None, scales=None):
         self.plan, self.sched = plan, sched
+        self.win, self.sumsq, self.scales = win, sumsq, scales
 
 
 class PivotSet:
@@ -128,11 +141,88 @@ class PivotSet:
         self.fv = torch.empty((len(counts), self.disp.nV, self.disp.nF), dtype=torch.float32, device=device)
         self.bytes_stack = [b.plan.algorithmic_bytes(out_rows=len(counts) * self.plan.R) for b in self.batches]
         self.host = (x_axis, t_axis, batch_trk[0])
+        for b in self.batches:
+            b.win, b.sumsq, b.scales = self.windows, self.sumsq, self.scales
+        self.units = self.n_total
+
+
+class SlidingSet:
+    """BASELINE configs[3]: a pool of long-fiber windows imaged at sliding pivots (UnitPlan).
+
+    Every batch gives the pool new per-pass trajectories (crossing point uniform along the fiber,
+    15-30 m/s, crossing at mid-window); a pass becomes one unit per pivot it crosses inside its
+    window (all rows with full-length slices on both sides).  Slots = speed class x pivot with
+    fixed class edges (20, 25 m/s), so that every rank's slots mean the same thing; the class means
+    use the GLOBAL unit count per slot (one all-reduce of the counts at setup)."""
+
+    def __init__(self, n_total, n_ch, n_t, seed, device, world, rank, opts, chunk=8):
+        from das_diff_veh_amd.plan import UnitPlan, sliding_pivots
+        from das_diff_veh_amd.vsg import flat_units, unit_sumsq
+        pool = opts["pool"]
+        self.n = pool
+        t0 = time.time()
+        self.windows, x_axis, t_axis, _, _ = synth_batch_device(
+            pool, n_ch=n_ch, n_t=n_t, pivot=n_ch * 8.16 / 2, seed=seed, device=device, x_first=0.37,
+            track_half=10, chunk=opts.get("gen_chunk", 2))
+        self.t_gen = time.time() - t0
+        t0 = time.time()
+        self.prm = VsgParams(wlen=2, norm=False, include_other_side=True)
+        edge = 4 * opts["pivot_every"]
+        pch = np.arange(edge, n_ch - edge, opts["pivot_every"])
+        n_piv = pch.size
+        rng = np.random.default_rng(seed + 7)
+        n_batch = -(-int(n_total) // pool)
+        self.n_total = n_batch * pool
+        sumsq = window_sumsq(self.windows)
+        plans, slot_l = [], []
+        for _ in range(n_batch):
+            x0 = rng.uniform(x_axis[edge], x_axis[-edge], pool)
+            v = rng.uniform(15.0, 30.0, pool)
+            tc = t_axis[n_t // 2] + rng.uniform(-1.0, 1.0, pool)
+            trk = []
+            for xa, va, ta in zip(x0, v, tc):
+                xs = np.arange(np.floor(xa) - 800.0, np.floor(xa) + 801.0)
+                trk.append((xs, np.round((ta + (xs - xa) / va) / TRACK_DT) * TRACK_DT))
+            plan = UnitPlan.sliding(x_axis, t_axis, trk, pch, opts["half_aperture"], self.prm)
+            cls = np.digitize(v[plan.unit_window], [20.0, 25.0])
+            plans.append(plan)
+            slot_l.append(cls * n_piv + plan.unit_pivot)
+        n_slot = 3 * n_piv
+        counts = np.bincount(np.concatenate(slot_l), minlength=n_slot)
+        if world > 1:
+            ct = torch.as_tensor(counts, dtype=torch.int64, device=device)
+            dist.all_reduce(ct)
+            counts = ct.cpu().numpy()
+        self.batches = []
+        for plan, sl in zip(plans, slot_l):
+            b = Batch(plan, StackSchedule(sl, n_slot, chunk=chunk, counts=counts), win=flat_units(self.windows, plan),
+                      sumsq=unit_sumsq(sumsq, plan),
+                      scales=torch.empty((plan.n_pass, 2), dtype=torch.float32, device=device))
+            self.batches.append(b)
+        self.units = sum(p.n_pass for p in plans)
+        self.plan = plans[0]
+        self.t_plan = time.time() - t0
+        R, w = self.plan.R, self.plan.w
+        dt = t_axis[1] - t_axis[0]
+        pv, st, en, _ = sliding_pivots(x_axis, pch[:1], opts["half_aperture"])
+        self.gx = x_axis[st[0]:en[0]] - x_axis[pv[0]]
+        self.gt = (np.arange(w) - w // 2) * dt
+        self.stack = torch.zeros((n_slot, R, w), dtype=torch.float32, device=device)
+        s = int(np.abs(self.gx - (-200.0)).argmin())
+        e = int(np.abs(self.gx - 0.0).argmin())
+        self.disp_rows = (s, e + 1)
+        self.disp = DispPlan(e + 1 - s, w, 8.16, dt, np.arange(0.8, 25, 0.1), np.arange(200, 1200))
+        self.fv = torch.empty((n_slot, self.disp.nV, self.disp.nF), dtype=torch.float32, device=device)
+        self.bytes_stack = [p.algorithmic_bytes(out_rows=n_slot * R) for p in plans]
+        self.host = None
 
 
 def build(workload, device, world, rank, chunk=8):
     sets, n_ch, n_t, desc, opts = WORKLOADS[workload]
     out = []
+    if opts.get("sliding"):
+        return [SlidingSet(sets[0][3], n_ch, n_t, seed=1000 * rank + 3, device=device, world=world, rank=rank,
+                           opts=opts, chunk=chunk)], desc
     for i, (pivot, sx, ex, counts) in enumerate(sets):
         out.append(PivotSet(pivot, sx, ex, counts, n_ch, n_t, seed=1000 * rank + 17 * i + 3, device=device,
                             world=world, rank=rank, opts=opts, chunk=chunk))
@@ -147,10 +237,10 @@ def step(sets, world, ev=None):
     k = 0
     for s in sets:
         for j, b in enumerate(s.batches):
-            vsg_scales(s.windows, b.plan, out=s.scales, win_sumsq=s.sumsq)
+            vsg_scales(b.win, b.plan, out=b.scales, win_sumsq=b.sumsq)
             if ev is not None:
                 ev[k][0].record()
-            vsg_stack(s.windows, b.plan, b.sched, scales=s.scales, out=s.stack, accumulate=j > 0)
+            vsg_stack(b.win, b.plan, b.sched, scales=b.scales, out=s.stack, accumulate=j > 0)
             if ev is not None:
                 ev[k][1].record()
             k += 1
@@ -330,6 +420,9 @@ def main():
                      "launch_ms": launch_s * 1e3},
         "host_index_tables_s": sum(s.t_plan for s in sets),
     }
+    res["config"]["gather_units_per_step_per_gpu"] = sum(s.units for s in sets)
+    if any(s.host is None for s in sets):
+        args.no_cpu_baseline = True  # the CPU loop images single-pivot windows (weights / speeds / synth10k)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(sets, args.cpu_budget)
         res["cpu_baseline"] = cb

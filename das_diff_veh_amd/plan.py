@@ -212,3 +212,156 @@ class VsgPlan:
             self._dev[key] = (torch.from_numpy(np.ascontiguousarray(self.pass_tab)).to(device),
                               torch.from_numpy(np.ascontiguousarray(self.seg_tab)).to(device))
         return self._dev[key]
+
+
+# ------------------------------------------------------------------------------------------------
+# Sliding pivots: one pass window imaged at many pivots along the fiber.
+#
+# The reference images a window at one pivot per VirtualShotGather call
+# (apis/virtual_shot_gather.py:183-192); sliding the pivot along the fiber is the caller looping
+# over pivots with start_x = pivot - a, end_x = pivot + a.  Here every (pass, pivot) pair is one
+# "unit" of a single launch.  The kernels address channel ch of unit u's window as
+# win + ch * ch_stride: with the windows [n, C, T] contiguous in (C, T), window q's channel c is
+# channel q * C + c of one flattened [n * C, T] record, so a unit carries row0 / pivot offset by
+# q * C and the launch sees pass_stride = 0 (das_diff_veh_amd.vsg.flat_units).  No ABI change.
+
+def sliding_pivots(x_axis, pivot_ch, half_aperture):
+    """Spatial indices of gathers centred on channels pivot_ch with start_x / end_x = pivot -/+ a:
+    (pivot_idx, start_idx, end_idx) arrays with the reference's expressions
+    (argmax(x >= pivot), argmax(x >= start_x), argmin|x - end_x|; preprocessing_window :111-126)."""
+    x_axis = np.asarray(x_axis, dtype=np.float64)
+    piv = x_axis[np.asarray(pivot_ch, dtype=np.int64)]
+    ge = lambda v: np.argmax(x_axis[None, :] >= v[:, None], axis=1)  # noqa: E731
+    return (ge(piv), ge(piv - half_aperture), np.abs(x_axis[None, :] - (piv + half_aperture)[:, None]).argmin(axis=1),
+            piv)
+
+
+def sliding_geometry(x_axis, t_axis, veh_state_x, veh_state_t, spatial, prm: VsgParams):
+    """seg tables of one pass at every pivot of ``spatial`` (from sliding_pivots), vectorised over
+    pivots and rows with pass_geometry's expressions (bit-identical tables: tests/test_host.py).
+
+    Returns (seg [J, R, 2, 2] int64, full [J] bool): ``full`` marks the pivots whose every row has
+    full-length time slices on both sides (the vehicle crosses the aperture inside the window)."""
+    x_axis = np.asarray(x_axis, dtype=np.float64)
+    t_axis = np.asarray(t_axis, dtype=np.float64)
+    pivot_idx, start_idx, end_idx, piv = spatial
+    R = int(end_idx[0] - start_idx[0])
+    if np.any(end_idx - start_idx != R):
+        raise ValueError("sliding pivots must share the gather row count")
+    f = interp1d_extrap(veh_state_x, veh_state_t)
+    dt = t_axis[1] - t_axis[0]
+    w = int(prm.wlen / dt)
+    nsamp = int(prm.time_window_to_xcorr // dt)
+    T = t_axis.size
+    rows = start_idx[:, None] + np.arange(R)[None, :]                  # [J, R]
+    # every expression is elementwise, so it is evaluated once per channel and gathered per
+    # (pivot, row): f(x[rows]) == f(x)[rows], f(pivot) == f(x)[pivot channel] (pivots sit on channels)
+    fx = f(x_axis)
+    fp = f(piv)
+    seg = np.zeros((len(piv), R, 2, 2), dtype=np.int64)
+    pt = first_true_ge(t_axis, fp + prm.delta_t)[:, None]
+    ti = first_true_ge(t_axis, fx + prm.delta_t)[rows]
+    shared = rows <= pivot_idx[:, None]
+    a = np.where(shared, pt, ti)
+    seg[:, :, 0, 0], seg[:, :, 0, 1] = py_slice(a, a + nsamp, T)
+    if prm.include_other_side:
+        pt = first_true_ge(t_axis, fp + (-prm.delta_t))[:, None]
+        ti = first_true_ge(t_axis, fx - prm.delta_t)[rows]
+        shared = rows >= pivot_idx[:, None]
+        b = np.where(shared, pt, ti)
+        seg[:, :, 1, 0], seg[:, :, 1, 1] = py_slice(b - nsamp, b, T)
+        full = np.all(seg[:, :, :, 1] == nsamp, axis=(1, 2))
+    else:
+        full = np.all(seg[:, :, 0, 1] == nsamp, axis=1)
+    if w < 2:
+        raise ValueError(f"correlation window too short: w={w}")
+    return seg, full
+
+
+def sliding_full(x_axis, t_axis, veh_state_x, veh_state_t, spatial, prm: VsgParams):
+    """sliding_geometry's ``full`` mask in O(C + J): per-channel slice lengths and prefix counts of
+    short slices, so that only the pivots a pass crosses get [R, 2, 2] tables."""
+    x_axis = np.asarray(x_axis, dtype=np.float64)
+    t_axis = np.asarray(t_axis, dtype=np.float64)
+    pivot_idx, start_idx, end_idx, piv = spatial
+    f = interp1d_extrap(veh_state_x, veh_state_t)
+    dt = t_axis[1] - t_axis[0]
+    nsamp = int(prm.time_window_to_xcorr // dt)
+    T = t_axis.size
+    fx, fp = f(x_axis), f(piv)
+
+    def short_prefix(ti, sgn):
+        a = ti if sgn > 0 else ti - nsamp
+        bad = (py_slice(a, a + nsamp, T)[1] != nsamp).astype(np.int64)
+        return np.concatenate([[0], np.cumsum(bad)])
+
+    def shared_ok(sgn):
+        pt = first_true_ge(t_axis, fp + sgn * prm.delta_t)
+        a = pt if sgn > 0 else pt - nsamp
+        return py_slice(a, a + nsamp, T)[1] == nsamp
+
+    cf = short_prefix(first_true_ge(t_axis, fx + prm.delta_t), 1)
+    full = shared_ok(1) & (cf[end_idx] - cf[pivot_idx + 1] == 0)          # forward rows pivot+1..end-1
+    if prm.include_other_side:
+        co = short_prefix(first_true_ge(t_axis, fx - prm.delta_t), -1)
+        full &= shared_ok(-1) & (co[pivot_idx] - co[start_idx] == 0)       # other-side rows start..pivot-1
+    return full
+
+
+class UnitPlan(VsgPlan):
+    """A launch over (window, pivot) units: VsgPlan tables with row0 / pivot offset by window * C.
+
+    ``unit_window[u]`` / ``unit_pivot[u]`` name each unit's window and pivot (index into the
+    spatial tables); ``n_ch`` of the plan is the flattened record's n * C channels."""
+
+    def __init__(self, seg_tab, unit_window, unit_pivot, spatial, prm: VsgParams, n_win, n_ch, n_t, dt, piv_ch=None):
+        pivot_idx, start_idx, end_idx, piv = spatial
+        self.R = int(end_idx[0] - start_idx[0])
+        self.w = int(prm.wlen / dt)
+        self.hop = int(self.w * (1 - 0.5))
+        self.nsamp = int(prm.time_window_to_xcorr // dt)
+        self.prm = prm
+        self.flags = prm.flags
+        self.unit_window = np.asarray(unit_window, dtype=np.int64)
+        self.unit_pivot = np.asarray(unit_pivot, dtype=np.int64)
+        self.n_pass = self.unit_window.size
+        if self.n_pass == 0:
+            raise ValueError("empty batch")
+        self.n_win, self.win_ch = int(n_win), int(n_ch)
+        self.pivots = np.asarray(piv_ch) if piv_ch is not None else None
+        self.n_ch, self.n_t = int(n_win) * int(n_ch), int(n_t)
+        off = self.unit_window * n_ch
+        self.pass_tab = np.stack([start_idx[self.unit_pivot] + off, pivot_idx[self.unit_pivot] + off],
+                                 axis=1).astype(np.int32)
+        self.seg_tab = np.ascontiguousarray(seg_tab, dtype=np.int32)
+        if self.n_ch >= 2 ** 31:
+            raise ValueError("flattened record exceeds int32 channel indices")
+        assert self.seg_tab.shape == (self.n_pass, self.R, 2, 2)
+        assert self.seg_tab.min() >= 0 and (self.seg_tab[..., 0] + self.seg_tab[..., 1]).max() <= n_t
+        self.geoms = None
+        self._dev = {}
+
+    @classmethod
+    def sliding(cls, x_axis, t_axis, trajectories, pivot_ch, half_aperture, prm: VsgParams, full_only=True):
+        """Units (q, j) for every window q (trajectories[q] = (veh_state_x, veh_state_t)) and pivot
+        channel pivot_ch[j]; with full_only only the pivots the vehicle crosses inside the window."""
+        spatial = sliding_pivots(x_axis, pivot_ch, half_aperture)
+        segs, uw, up = [], [], []
+        for q, (vx, vt) in enumerate(trajectories):
+            if full_only:
+                j = np.nonzero(sliding_full(x_axis, t_axis, vx, vt, spatial, prm))[0]
+                if j.size == 0:
+                    segs.append(np.zeros((0, int(spatial[2][0] - spatial[1][0]), 2, 2), dtype=np.int64))
+                    continue
+                seg = sliding_geometry(x_axis, t_axis, vx, vt, tuple(a[j] for a in spatial), prm)[0]
+            else:
+                j = np.arange(spatial[0].size)
+                seg = sliding_geometry(x_axis, t_axis, vx, vt, spatial, prm)[0]
+            segs.append(seg)
+            uw.append(np.full(j.size, q))
+            up.append(j)
+        if not uw:
+            raise ValueError("empty batch: no pass crosses a pivot inside its window")
+        t_axis = np.asarray(t_axis, dtype=np.float64)
+        return cls(np.concatenate(segs), np.concatenate(uw), np.concatenate(up), spatial, prm, len(trajectories),
+                   len(x_axis), t_axis.size, t_axis[1] - t_axis[0], piv_ch=pivot_ch)

@@ -123,3 +123,25 @@ def vsg_stack(windows: torch.Tensor, plan: VsgPlan, schedule: StackSchedule, sca
               _lib.ptr(order), _lib.ptr(chunk_tab), int(chunk_tab.shape[0]), _lib.ptr(weights), _lib.ptr(out),
               _lib.stream_of(windows.device))
     return out
+
+
+def flat_units(windows: torch.Tensor, plan) -> torch.Tensor:
+    """The launch view of a UnitPlan (plan.UnitPlan): windows [n, C, T] with contiguous (C, T) seen
+    as n_unit copies of one flattened [n * C, T] record (pass stride 0); the plan's row0 / pivot
+    already carry each unit's window offset q * C."""
+    if not windows.is_cuda or windows.dtype != torch.float32 or windows.dim() != 3:
+        raise ValueError("windows must be a float32 device tensor [n, C, T]")
+    n, C, T = windows.shape
+    if (n, C) != (plan.n_win, plan.win_ch) or T < plan.n_t:
+        raise ValueError(f"windows {tuple(windows.shape)} do not match the plan ({plan.n_win}, {plan.win_ch}, {plan.n_t})")
+    if windows.stride(2) != 1 or windows.stride(0) != C * windows.stride(1):
+        raise ValueError("unit launches need windows contiguous in (channel, time)")
+    return windows.as_strided((plan.n_pass, n * C, T), (0, windows.stride(1), 1))
+
+
+def unit_sumsq(win_sumsq: torch.Tensor, plan) -> torch.Tensor:
+    """Per-unit ||window||_F^2 from the per-window values (window_sumsq of the [n, C, T] windows)."""
+    key = ("unit_window", str(win_sumsq.device))
+    if key not in plan._dev:
+        plan._dev[key] = torch.from_numpy(plan.unit_window).to(win_sumsq.device)
+    return win_sumsq.index_select(0, plan._dev[key])

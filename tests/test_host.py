@@ -203,3 +203,45 @@ def test_pass_table_untracked_crossing_raises():
     vs[2, c["x0"] - c["start_x_tracking"]] = np.nan
     with pytest.raises(ValueError):
         pass_table(c["t_axis"], c["dist"], c["x0"], c["start_x_tracking"], vs, c["t_trk"], 0.004, wlen_sw=2)
+
+
+def _sliding_case(n_ch=300, n_t=8192, seed=5):
+    from das_diff_veh_amd.synth import TRACK_DT, DT_W500
+    rng = np.random.default_rng(seed)
+    x_axis = 0.37 + 8.16 * np.arange(n_ch)
+    t_axis = DT_W500 + np.arange(n_t) * 0.004
+    trk = []
+    for _ in range(4):
+        x0, v = rng.uniform(600, 1800), rng.uniform(15, 30)
+        tc = t_axis[n_t // 2] + rng.uniform(-1, 1)
+        xs = np.arange(np.floor(x0) - 1500, np.floor(x0) + 1500, 1.0)
+        trk.append((xs, np.round((tc + (xs - x0) / v) / TRACK_DT) * TRACK_DT))
+    return x_axis, t_axis, trk
+
+
+def test_sliding_geometry_matches_pass_geometry():
+    """Vectorised sliding-pivot tables == pass_geometry at each pivot (start_x / end_x = pivot -/+ 200)."""
+    from das_diff_veh_amd.plan import (UnitPlan, VsgParams, pass_geometry, sliding_full, sliding_geometry,
+                                       sliding_pivots)
+    x_axis, t_axis, trk = _sliding_case()
+    pch = np.arange(32, 300 - 32, 8)
+    prm = VsgParams(include_other_side=True, norm=False)
+    spatial = sliding_pivots(x_axis, pch, 200.0)
+    n_full = 0
+    for vx, vt in trk:
+        seg, full = sliding_geometry(x_axis, t_axis, vx, vt, spatial, prm)
+        assert np.array_equal(full, sliding_full(x_axis, t_axis, vx, vt, spatial, prm))
+        n_full += int(full.sum())
+        for j, c in enumerate(pch):
+            p = float(x_axis[c])
+            g = pass_geometry(x_axis, t_axis, vx, vt, VsgParams(pivot=p, start_x=p - 200.0, end_x=p + 200.0,
+                                                                  include_other_side=True, norm=False))
+            assert (g.pivot_idx, g.start_idx, g.end_idx) == (spatial[0][j], spatial[1][j], spatial[2][j])
+            assert np.array_equal(g.seg, seg[j]), j
+            assert full[j] == bool(np.all(g.seg[:, :, 1] == g.nsamp))
+    assert n_full > 0
+    plan = UnitPlan.sliding(x_axis, t_axis, trk, pch, 200.0, prm)
+    assert plan.n_pass == n_full and plan.R == 49
+    # unit u reads window q's channels at q * C + c of the flattened record
+    q, j = plan.unit_window[3], plan.unit_pivot[3]
+    assert plan.pass_tab[3, 1] == q * 300 + spatial[0][j]

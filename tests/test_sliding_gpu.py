@@ -1,0 +1,94 @@
+"""GPU parity of sliding-pivot launches: one launch images every
+(pass, pivot) unit, pivots every 8 channels with start_x / end_x = pivot -/+ 200 m, each unit
+checked against the oracle's VirtualShotGather at that pivot (apis/virtual_shot_gather.py:183-192)."""
+import numpy as np
+import pytest
+
+from tests import golden_io as gio
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def _case(device, n=3, n_ch=300, n_t=8192, seed=11):
+    from das_diff_veh_amd.synth import synth_batch_device
+    w, x, t, trk, _ = synth_batch_device(n, n_ch=n_ch, n_t=n_t, pivot=1224.0, seed=seed, device=device,
+                                         x_first=0.37, track_half=1500, chunk=1)
+    return w, x, t, trk
+
+
+def _oracle_unit(host, x, t, trk, plan, u, kw):
+    from oracle import vsg as ovsg
+    q, j = int(plan.unit_window[u]), int(plan.unit_pivot[u])
+    p = float(x[plan.pivots[j]])
+    o = dict(data=host[q], x_axis=x, t_axis=t, veh_state_x=trk[q][0], veh_state_t=trk[q][1])
+    return ovsg.virtual_shot_gather(o, pivot=p, start_x=p - 200.0, end_x=p + 200.0, wlen=2, **kw)[0]
+
+
+@pytest.mark.parametrize("kw", [dict(include_other_side=True, norm=False), dict(include_other_side=True),
+                                dict(include_other_side=False, norm=False)])
+def test_sliding_unit_gathers(device, kw):
+    _check_gathers(device, kw, full_only=True, n=8)
+
+
+@pytest.mark.parametrize("kw", [dict(include_other_side=True, norm=False), dict(include_other_side=True)])
+def test_sliding_all_pivots(device, kw):
+    """Every pivot, including those whose trajectory slices leave the window (short / empty
+    sub-window sets, all-zero sides -> the reference's zeros and 0/0 NaNs)."""
+    _check_gathers(device, kw, full_only=False, n=3)
+
+
+def _check_gathers(device, kw, full_only, n):
+    from das_diff_veh_amd import vsg
+    from das_diff_veh_amd.plan import UnitPlan, VsgParams
+    w, x, t, trk = _case(device, n=n)
+    prm = VsgParams(**kw)
+    pch = np.arange(32, w.shape[1] - 32, 8)
+    plan = UnitPlan.sliding(x, t, trk, pch, 200.0, prm, full_only=full_only)
+    assert plan.n_pass >= (6 if full_only else n * len(pch))
+    flat = vsg.flat_units(w, plan)
+    sc = vsg.vsg_scales(flat, plan, win_sumsq=vsg.unit_sumsq(vsg.window_sumsq(w), plan))
+    got = vsg.vsg_gathers(flat, plan, sc).double().cpu().numpy()
+    host = w.double().cpu().numpy()
+    finite_scale = np.isfinite(sc.cpu().numpy()).all(axis=1)
+    for u in range(plan.n_pass):
+        with np.errstate(all="ignore"):
+            ref = _oracle_unit(host, x, t, trk, plan, u, kw)
+        if finite_scale[u]:
+            assert gio.gather_rel_err(got[u], ref) < TOL, (u, kw)
+        else:
+            # a side whose pivot slice is empty (Python-slice wrap at the window start) has
+            # amax(pivot row) = 0: the reference's x / 0 gives +-inf with the sign of x, and for
+            # correlations that are 0 up to rounding that sign is rounding noise (fp32 vs float64),
+            # so only the finite / NaN / inf positions are compared
+            assert not full_only
+            assert np.array_equal(np.isnan(got[u]), np.isnan(ref)) and np.array_equal(np.isinf(got[u]), np.isinf(ref))
+            m = np.isfinite(ref)
+            assert gio.gather_rel_err(np.where(m, got[u], 0.0), np.where(m, ref, 0.0)) < TOL, u
+
+
+def test_sliding_class_stacks(device):
+    """Per-(class, pivot) stacks of one launch == the oracle's mean of that pivot's unit gathers."""
+    from das_diff_veh_amd import vsg
+    from das_diff_veh_amd.plan import UnitPlan, VsgParams
+    from oracle import vsg as ovsg
+    w, x, t, trk = _case(device, n=4, seed=12)
+    kw = dict(include_other_side=True, norm=False)
+    pch = np.arange(32, w.shape[1] - 32, 8)
+    plan = UnitPlan.sliding(x, t, trk, pch, 200.0, VsgParams(**kw))
+    cls = plan.unit_window % 2
+    slots = cls * len(pch) + plan.unit_pivot
+    n_slot = 2 * len(pch)
+    flat = vsg.flat_units(w, plan)
+    sched = vsg.StackSchedule(slots, n_slot, chunk=2)
+    got = vsg.vsg_stack(flat, plan, sched, win_sumsq=vsg.unit_sumsq(vsg.window_sumsq(w), plan))
+    got = got.double().cpu().numpy()
+    host = w.double().cpu().numpy()
+    checked = 0
+    for s in np.unique(slots):
+        units = np.flatnonzero(slots == s)
+        ref = ovsg.stack([_oracle_unit(host, x, t, trk, plan, u, kw) for u in units])
+        assert gio.gather_rel_err(got[s], ref) < TOL, s
+        checked += 1
+    empty = np.setdiff1d(np.arange(n_slot), slots)
+    assert np.all(got[empty] == 0.0) and checked >= 4
