@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "dvh_common.h"
 #include "dvh.h"
@@ -202,6 +203,202 @@ __global__ __launch_bounds__(256) void fv_kernel(const double* __restrict__ FK, 
   }
 }
 
+// 3b. Batched f-v sampling (many images of one plan): one 1024-thread block = (VC velocities, all
+// frequencies) x G consecutive images.  The bilinear weights depend on (f, v) only, so each thread
+// computes them ONCE (frequency f = tid % nF, velocities 4 g .. 4 g + 3 of the chunk, g = tid / nF)
+// and keeps them in registers across the G images.  Per image: the image's FK grid is staged in LDS
+// (n_kb x n_fb doubles), the float32 samples go to an LDS row per velocity padded by kSgPad zeros on
+// both sides, and the Savitzky-Golay pass gives every thread 4 consecutive outputs of one velocity
+// (28 inputs read as 7 x 16 B, 25 taps each in double, the same tap order as fv_kernel).  Bound:
+// float64 FMA issue (25 per output) and the 4 B/output HBM write.
+#ifndef DVH_FV_LEGACY
+#define DVH_FV_LEGACY 0  // 1: always the per-image fv_kernel (A/B builds)
+#endif
+#ifndef DVH_FV_BATCH
+#define DVH_FV_BATCH 0   // default dispatch of the batched kernel (DVH_FV_G=<images per block> selects it at run time)
+#endif
+constexpr int kFvThreads = 1024;
+constexpr int kFvVT = 4;   // velocities per thread in the sampling phase
+constexpr int kFvPre = 4;  // FK doubles prefetched per thread: grids up to 4 x 1024 bins
+constexpr int kSgPad = 12; // zero pad per side of an LDS row (the fast path needs sgl = 2 * kSgPad + 1)
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also orders global memory (a
+// workgroup-scope release: s_waitcnt vmcnt(0)), which would stall every image on the previous
+// image's f-v stores; the fv stores are never read back by the block.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ int fv_row_stride(int nF) { return ((nF + 3) & ~3) + 2 * kSgPad; }
+
+__global__ __launch_bounds__(kFvThreads) void fv_batch_kernel(
+    const double* __restrict__ FK, int32_t B, int32_t G, int32_t n_kb, int32_t n_fb,
+    const double* __restrict__ kgrid, double kmin, double kmax, const double* __restrict__ kq, int32_t nF,
+    int32_t nV, int32_t n_grp, const int32_t* __restrict__ fj, const double* __restrict__ fw,
+    const double* __restrict__ sg, int32_t sgl, float* __restrict__ fv) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int nfk = n_kb * n_fb;
+  const int nfk2 = (nfk + 1) & ~1;
+  double* fks = smem;                                                // 2 x [n_kb][n_fb] (double buffer)
+  const int VC = kFvVT * n_grp, S = fv_row_stride(nF);
+  double* sgs = smem + 2 * nfk2;                                     // Savitzky-Golay taps + edge fits
+  float* raw = reinterpret_cast<float*>(sgs + ((sgl * sgl + 1) & ~1));  // [VC][S], x[f] at kSgPad + f
+  const int v0 = blockIdx.x * VC, tid = threadIdx.x;
+
+  // sampling ownership and weights (fv_kernel's expressions, computed once)
+  const int g = tid / nF, f = tid - g * nF;
+  const bool own = g < n_grp;
+  int base[kFvVT];
+  double hx0[kFvVT], hx1[kFvVT], hy0 = 0.0, hy1 = 0.0;
+  {
+    const double k0 = kgrid[0], inv_dk = 1.0 / (kgrid[1] - kgrid[0]);
+    const int j = own ? fj[f] : 0;
+    if (own) {
+      hy0 = fw[2 * f];
+      hy1 = fw[2 * f + 1];
+    }
+#pragma unroll
+    for (int i = 0; i < kFvVT; ++i) {
+      const int v = v0 + kFvVT * g + i;
+      base[i] = -1;
+      hx0[i] = hx1[i] = 0.0;
+      if (own && v < nV) {
+        double q = kq[(int64_t)f * nV + v];
+        q = q < kmin ? kmin : (q > kmax ? kmax : q);
+        int m = (int)floor((q - k0) * inv_dk);
+        m = m < 0 ? 0 : (m > n_kb - 2 ? n_kb - 2 : m);
+        while (m < n_kb - 2 && q >= kgrid[m + 1]) ++m;
+        while (m > 0 && q < kgrid[m]) --m;
+        const double klo = kgrid[m], khi = kgrid[m + 1];
+        const double fx = 1.0 / (khi - klo);
+        hx0[i] = fx * (khi - q);
+        hx1[i] = fx * (q - klo);
+        base[i] = m * n_fb + j;
+      }
+    }
+  }
+  // zero pads (never written afterwards)
+  for (int e = tid; e < VC * S; e += kFvThreads) {
+    const int c = e % S;
+    if (c < kSgPad || c >= kSgPad + nF) raw[e] = 0.f;
+  }
+  const int half = sgl / 2;
+  for (int e = tid; e < sgl * sgl; e += kFvThreads) sgs[e] = sg[e];  // sgl + 2 * half * sgl = sgl^2 entries
+  const double* h = sgs;
+  const double* el = sgs + sgl;
+  const double* er = el + half * sgl;
+  const int nb4 = (nF + 3) >> 2;
+  const bool fast_taps = (sgl == 2 * kSgPad + 1);
+  // FK grids are software-pipelined: image it + 1's grid is loaded into registers (kFvPre per
+  // thread) while image it is sampled, and stored to the other LDS buffer before its filter pass
+  const int b0 = blockIdx.y * G;
+  const int n_img = min(G, B - b0);
+  double pre[kFvPre];
+#pragma unroll
+  for (int k = 0; k < kFvPre; ++k) {
+    const int e = tid + k * kFvThreads;
+    if (e < nfk) fks[e] = FK[(int64_t)b0 * nfk + e];
+  }
+  for (int it = 0; it < n_img; ++it) {
+    const int b = b0 + it;
+    const double* fk_cur = fks + (it & 1) * nfk2;
+    lds_barrier();  // fk_cur stored, raw free
+    const bool more = it + 1 < n_img;
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < kFvPre; ++k) {
+        const int e = min(tid + k * kFvThreads, nfk - 1);  // unconditional load: no register zeroing
+        pre[k] = FK[(int64_t)(b + 1) * nfk + e];
+      }
+    }
+    if (own) {
+#pragma unroll
+      for (int i = 0; i < kFvVT; ++i) {
+        if (base[i] < 0) continue;
+        const int m = base[i];
+        const double z00 = fk_cur[m], z01 = fk_cur[m + 1], z10 = fk_cur[m + n_fb], z11 = fk_cur[m + n_fb + 1];
+        raw[(kFvVT * g + i) * S + kSgPad + f] =
+            (float)(z00 * hx0[i] * hy0 + z01 * hx0[i] * hy1 + z10 * hx1[i] * hy0 + z11 * hx1[i] * hy1);
+      }
+    }
+    if (more) {  // next image's grid -> the other LDS buffer (read last in the previous image's phase 1)
+      double* fk_next = fks + ((it + 1) & 1) * nfk2;
+#pragma unroll
+      for (int k = 0; k < kFvPre; ++k) {
+        const int e = tid + k * kFvThreads;
+        if (e < nfk) fk_next[e] = pre[k];
+      }
+    }
+    lds_barrier();
+    for (int task = tid; task < VC * nb4; task += kFvThreads) {
+      const int r = task / nb4, f0 = (task - r * nb4) * 4, v = v0 + r;
+      if (v >= nV) continue;
+      const float* row = raw + r * S + kSgPad;  // row[x] = sample at frequency x (zero outside [0, nF))
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      if (fast_taps && f0 >= half && f0 + 3 < nF - half) {
+        float x[28];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+          const float4 t4 = *reinterpret_cast<const float4*>(row + f0 - kSgPad + 4 * q);
+          x[4 * q] = t4.x; x[4 * q + 1] = t4.y; x[4 * q + 2] = t4.z; x[4 * q + 3] = t4.w;
+        }
+#pragma unroll
+        for (int t = 0; t < 2 * kSgPad + 1; ++t) {
+          const double ht = sg[t];  // uniform: scalar loads, SGPR operands
+#pragma unroll
+          for (int o = 0; o < 4; ++o) acc[o] += ht * (double)x[o + t];
+        }
+      } else if (fast_taps) {
+        // edge block: the edge fits read x[0, 25) or x[nF - 25, nF) -- loaded once, all loops
+        // unrolled so the LDS reads are batched (a rolled loop here stalls the whole block at the
+        // next barrier: one dependent LDS round trip per tap)
+        constexpr int L = 2 * kSgPad + 1;
+        const float* src = f0 < half ? row : row + nF - L;
+        float y[L];
+#pragma unroll
+        for (int t = 0; t < L; ++t) y[t] = src[t];
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          const int ff = f0 + o;
+          if (ff >= nF) break;
+          double a = 0.0;
+          if (ff < half || ff >= nF - half) {
+            const double* c = ff < half ? el + ff * L : er + (ff - (nF - half)) * L;
+#pragma unroll
+            for (int t = 0; t < L; ++t) a += c[t] * (double)y[t];
+          } else {
+#pragma unroll
+            for (int t = 0; t < L; ++t) a += sg[t] * (double)row[ff - half + t];
+          }
+          acc[o] = a;
+        }
+      } else {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          const int ff = f0 + o;
+          if (ff >= nF) break;
+          double a = 0.0;
+          if (ff < half) {
+            for (int t = 0; t < sgl; ++t) a += el[ff * sgl + t] * (double)row[t];
+          } else if (ff >= nF - half) {
+            const int rr = ff - (nF - half);
+            for (int t = 0; t < sgl; ++t) a += er[rr * sgl + t] * (double)row[nF - sgl + t];
+          } else {
+            for (int t = 0; t < sgl; ++t) a += h[t] * (double)row[ff - half + t];
+          }
+          acc[o] = a;
+        }
+      }
+      float* out = fv + ((int64_t)b * nV + v) * nF + f0;
+      if ((nF & 3) == 0) {
+        *reinterpret_cast<float4*>(out) = make_float4((float)acc[0], (float)acc[1], (float)acc[2], (float)acc[3]);
+      } else {
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+          if (f0 + o < nF) out[o] = (float)acc[o];
+      }
+    }
+  }
+}
+
 // per-row L1 norms -> 1 / ||row||_1 (map_fv norm=True: data / norm(data, ord=1, axis=-1))
 __global__ __launch_bounds__(256) void row_l1_kernel(const float* __restrict__ data, int64_t b_stride,
                                                       int64_t ch_stride, int32_t nch, int32_t nt,
@@ -282,6 +479,31 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
   if (n_kb < 2 || n_fb < 2) return set_error(-2, "FK grid needs at least 2 x 2 bins");
   if (sgl % 2 == 0 || sgl > nF) return set_error(-4, "savgol window must be odd and <= number of frequencies");
   if (B <= 0 || nV <= 0) return 0;
+  // batched kernel: weights computed once per (f, v) and reused over G images of the block
+  int n_grp = nF <= kFvThreads ? kFvThreads / nF : 0;
+  n_grp = n_grp > 8 ? 8 : n_grp;
+  if (!DVH_FV_LEGACY && n_grp > 0) {
+    const int VC = kFvVT * n_grp;
+    const size_t lds_b = 2 * sizeof(double) * (size_t)(((size_t)n_kb * n_fb + 1) & ~(size_t)1) +
+                         sizeof(double) * (size_t)((sgl * sgl + 1) & ~1) + sizeof(float) * (size_t)VC * (((nF + 3) & ~3) + 2 * kSgPad);
+    if ((int64_t)n_kb * n_fb <= (int64_t)kFvPre * kFvThreads && lds_b <= 150 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)fv_batch_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds_b);
+      if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+      const int nvc = (nV + VC - 1) / VC;
+      // images per block: enough blocks to fill the chip (>= ~2048), at most 16 images each
+      int G = (int)(((int64_t)B * nvc + 2047) / 2048);
+      G = G < 1 ? 1 : (G > 16 ? 16 : G);
+      if (!DVH_FV_BATCH) G = 0;
+      if (const char* ev = getenv("DVH_FV_G")) G = atoi(ev);  // A/B: images per block (0: per-image kernel)
+      if (G > 0) {
+      dim3 grid(nvc, (B + G - 1) / G);
+      hipLaunchKernelGGL(fv_batch_kernel, grid, dim3(kFvThreads), lds_b, (hipStream_t)stream, FK, B, G, n_kb, n_fb,
+                         kgrid, kmin, kmax, kq, nF, nV, n_grp, fj, fw, sg, sgl, fv);
+      return last_launch();
+      }
+    }
+  }
   const size_t lds = sizeof(float) * (size_t)nF * kVS;
   if (lds > 160 * 1024) return set_error(-4, "too many frequencies for one block");
   hipError_t e = hipFuncSetAttribute((const void*)fv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -118,3 +118,21 @@ def synth_batch_device(n_pass, n_ch=60, n_t=5500, dx=8.16, x_first=None, t0=DT_W
         t = tc + (xs_trk - pivot) / v
         trk.append((xs_trk, np.round(t / TRACK_DT) * TRACK_DT))
     return out, x_axis, t_axis, trk, speeds
+
+
+def synth_gathers(B, nch, nt, dx, dt, device, seed=0):
+    """B gather-shaped [nch, nt] float32 blocks on the device (offsets 0, -dx, ...; lags centred):
+    12 dispersive tones c(f) with random phases under a 0.6 s Gaussian lag envelope, plus noise --
+    stand-ins for class-stack gathers in dispersion throughput and parity runs."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    x = -dx * torch.arange(nch, device=device, dtype=torch.float64)[:, None]
+    t = (torch.arange(nt, device=device, dtype=torch.float64) - nt // 2)[None, :] * dt
+    out = torch.zeros((B, nch, nt), dtype=torch.float64, device=device)
+    rng = np.random.default_rng(seed)
+    for f in rng.uniform(2.0, 24.0, 12):
+        ph = torch.rand((B, 1, 1), generator=g, device=device, dtype=torch.float64) * 2 * np.pi
+        out += torch.cos(2 * np.pi * f * (t + x / phase_velocity(f)) + ph) * torch.exp(-(t / 0.6) ** 2)
+    out += 0.05 * torch.randn((B, nch, nt), generator=g, device=device, dtype=torch.float64)
+    return out.float().contiguous()

@@ -1,0 +1,29 @@
+"""GPU parity of the batched f-v sampling kernel (fv_batch_kernel) on BASELINE configs[4]'s grid:
+512 velocities x 1,000 frequencies, many images per launch (weights reused across the images of a
+block), against the oracle's map_fv (modules/utils.py:457-475): rel-err <= 1e-4, picks per the
+SURVEY §8(d) tie rule."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+@pytest.mark.parametrize("G", [None, "3", "16"])
+@pytest.mark.parametrize("B,nv,nf", [(40, 512, 1000), (7, 300, 242), (5, 64, 1001)])
+def test_fv_batch_vs_oracle(device, monkeypatch, B, nv, nf, G):
+    """G: images per block of the batched kernel (DVH_FV_G, read at each launch); None = default dispatch."""
+    if G is not None:
+        monkeypatch.setenv("DVH_FV_G", G)
+    from das_diff_veh_amd.disp import DispPlan, fv_maps
+    from das_diff_veh_amd.synth import synth_gathers
+    from oracle import disp as odisp
+    nch, nt, dx, dt = 25, 500, 8.16, 0.003999999999997783
+    freqs, vels = np.linspace(1.0, 25.0, nf), np.linspace(200.0, 1200.0, nv)
+    data = synth_gathers(B, nch, nt, dx, dt, device, seed=B)
+    got = fv_maps(data, DispPlan(nch, nt, dx, dt, freqs, vels)).double().cpu().numpy()
+    host = data.double().cpu().numpy()
+    for b in sorted({0, 1, B // 2, B - 1}):
+        ref = odisp.map_fv(host[b], dx, dt, freqs, vels)
+        assert np.abs(got[b] - ref).max() / np.abs(ref).max() < TOL, b
+        assert np.all(odisp.pick_ok(ref, got[b].argmax(axis=0))), b
