@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void fv_kernel(const double* __restrict__ FK, 
 #define DVH_FV_LEGACY 0  // 1: always the per-image fv_kernel (A/B builds)
 #endif
 #ifndef DVH_FV_BATCH
-#define DVH_FV_BATCH 0   // default dispatch of the batched kernel (DVH_FV_G=<images per block> selects it at run time)
+#define DVH_FV_BATCH 1   // default dispatch of the batched kernel (DVH_FV_G=<images per block> selects it at run time)
 #endif
 constexpr int kFvThreads = 1024;
 constexpr int kFvVT = 4;   // velocities per thread in the sampling phase
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kFvThreads) void fv_batch_kernel(
             (float)(z00 * hx0[i] * hy0 + z01 * hx0[i] * hy1 + z10 * hx1[i] * hy0 + z11 * hx1[i] * hy1);
       }
     }
-    if (more) {  // next image's grid -> the other LDS buffer (read last in the previous image's phase 1)
+    if (more) {  // next image's grid -> the other LDS buffer (last read in the previous image's sampling)
       double* fk_next = fks + ((it + 1) & 1) * nfk2;
 #pragma unroll
       for (int k = 0; k < kFvPre; ++k) {
@@ -492,9 +492,12 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
       if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
       const int nvc = (nV + VC - 1) / VC;
       // images per block: enough blocks to fill the chip (>= ~2048), at most 16 images each
-      int G = (int)(((int64_t)B * nvc + 2047) / 2048);
-      G = G < 1 ? 1 : (G > 16 ? 16 : G);
-      if (!DVH_FV_BATCH) G = 0;
+      // images per block: 1 024 blocks (4 per CU) amortise the per-block weights best (measured
+      // G = 64 > 16 > 4 on 512 images of 512 x 1000); below ~1 024 (v-chunk, image) pairs the
+      // per-image kernel's 256-thread blocks fill the chip better
+      int G = (int)(((int64_t)B * nvc + 1023) / 1024);
+      G = G < 1 ? 1 : (G > 64 ? 64 : G);
+      if (!DVH_FV_BATCH || (int64_t)B * nvc < 1024) G = 0;
       if (const char* ev = getenv("DVH_FV_G")) G = atoi(ev);  // A/B: images per block (0: per-image kernel)
       if (G > 0) {
       dim3 grid(nvc, (B + G - 1) / G);
