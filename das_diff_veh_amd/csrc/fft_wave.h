@@ -32,12 +32,22 @@ __device__ __forceinline__ float2 lds_ld(const float2* p, int idx) {
 
 namespace dvh {
 
+typedef float pk2 __attribute__((ext_vector_type(2)));
+#ifndef DVH_PK_BFLY
+#define DVH_PK_BFLY 0  // 1: butterfly adds / constant multiplies as packed f32 vector ops (v_pk_*_f32)
+#endif
+#if DVH_PK_BFLY
+__device__ __forceinline__ pk2 vp(float2 a) { return __builtin_bit_cast(pk2, a); }
+__device__ __forceinline__ float2 fp(pk2 a) { return __builtin_bit_cast(float2, a); }
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return fp(vp(a) + vp(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return fp(vp(a) - vp(b)); }
+#else
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+#endif
 #ifndef DVH_PK_CMUL
 #define DVH_PK_CMUL 0
 #endif
-typedef float pk2 __attribute__((ext_vector_type(2)));
 // a * b.  Default (0): plain C.  1: two packed ops (v_pk_mul_f32, then v_pk_fma_f32 with operand
 // selects / negation); 2: four scalar ops in asm.  Measured on the N = 500 stack kernel: packed
 // forms are no faster than scalar FMAs on gfx950 (1 was 2-3 % slower), so the default stays C.
@@ -59,10 +69,31 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 #endif
 }
+#if DVH_PK_BFLY
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return fp(vp(a) * s); }
+#else
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+#endif
 // -i * a and +i * a
 __device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
 __device__ __forceinline__ float2 mul_pi(float2 a) { return make_float2(-a.y, a.x); }
+// m + (-i) u = (m.x + u.y, m.y - u.x) and m + i u = (m.x - u.y, m.y + u.x)
+#if DVH_PK_BFLY
+// one v_pk_add_f32 each: the swap and the negation ride on op_sel / neg modifiers
+__device__ __forceinline__ float2 add_mi(float2 m, float2 u) {
+  pk2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(vp(m)), "v"(vp(u)));
+  return fp(r);
+}
+__device__ __forceinline__ float2 add_pi(float2 m, float2 u) {
+  pk2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(vp(m)), "v"(vp(u)));
+  return fp(r);
+}
+#else
+__device__ __forceinline__ float2 add_mi(float2 m, float2 u) { return cadd(m, mul_mi(u)); }
+__device__ __forceinline__ float2 add_pi(float2 m, float2 u) { return cadd(m, mul_pi(u)); }
+#endif
 
 // Orders this wave's LDS accesses across lanes (a single wave executes LDS ops in order; the
 // fences stop the compiler from moving loads/stores across the stage boundary).
@@ -90,8 +121,8 @@ template <> struct Dft<3> {
     const float2 m = make_float2(a[0].x + c * t.x, a[0].y + c * t.y);
     const float2 u = cscale(d, s);
     a[0] = cadd(a[0], t);
-    a[1] = cadd(m, mul_mi(u));
-    a[2] = cadd(m, mul_pi(u));
+    a[1] = add_mi(m, u);
+    a[2] = add_pi(m, u);
   }
 };
 
@@ -101,8 +132,8 @@ template <> struct Dft<4> {
     const float2 s13 = cadd(a[1], a[3]), d13 = csub(a[1], a[3]);
     a[0] = cadd(s02, s13);
     a[2] = csub(s02, s13);
-    a[1] = cadd(d02, mul_mi(d13));
-    a[3] = csub(d02, mul_mi(d13));
+    a[1] = add_mi(d02, d13);
+    a[3] = add_pi(d02, d13);
   }
 };
 
@@ -112,15 +143,22 @@ template <> struct Dft<5> {
     constexpr float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
     const float2 t1 = cadd(a[1], a[4]), t2 = cadd(a[2], a[3]);
     const float2 t3 = csub(a[1], a[4]), t4 = csub(a[2], a[3]);
+#if DVH_PK_BFLY
+    const float2 m1 = fp(vp(a[0]) + c1 * vp(t1) + c2 * vp(t2));
+    const float2 m2 = fp(vp(a[0]) + c2 * vp(t1) + c1 * vp(t2));
+    const float2 u1 = fp(s1 * vp(t3) + s2 * vp(t4));
+    const float2 u2 = fp(s2 * vp(t3) - s1 * vp(t4));
+#else
     const float2 m1 = make_float2(a[0].x + c1 * t1.x + c2 * t2.x, a[0].y + c1 * t1.y + c2 * t2.y);
     const float2 m2 = make_float2(a[0].x + c2 * t1.x + c1 * t2.x, a[0].y + c2 * t1.y + c1 * t2.y);
     const float2 u1 = make_float2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y);
     const float2 u2 = make_float2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y);
+#endif
     a[0] = cadd(a[0], cadd(t1, t2));
-    a[1] = cadd(m1, mul_mi(u1));
-    a[4] = cadd(m1, mul_pi(u1));
-    a[2] = cadd(m2, mul_mi(u2));
-    a[3] = cadd(m2, mul_pi(u2));
+    a[1] = add_mi(m1, u1);
+    a[4] = add_pi(m1, u1);
+    a[2] = add_mi(m2, u2);
+    a[3] = add_pi(m2, u2);
   }
 };
 
