@@ -222,6 +222,9 @@ __global__ __launch_bounds__(256) void fv_kernel(const double* __restrict__ FK, 
 #ifndef DVH_FV_LEGACY
 #define DVH_FV_LEGACY 0  // 1: always the per-image fv_kernel (A/B builds)
 #endif
+#ifndef DVH_FV_TILE
+#define DVH_FV_TILE 1    // default: the frequency-tiled kernel (DVH_FV_TILE=0 at run time selects the others)
+#endif
 #ifndef DVH_FV_BATCH
 #define DVH_FV_BATCH 1   // default dispatch of the batched kernel (DVH_FV_G=<images per block> selects it at run time)
 #endif
@@ -407,6 +410,172 @@ __global__ __launch_bounds__(kFvThreads) void fv_batch_kernel(
   }
 }
 
+// 3c. Frequency-tiled f-v sampling: one 256-thread block = (a tile of TO output frequencies, 4
+// velocities) x G images, so that several independent blocks share a CU (the 1 024-thread
+// fv_batch_kernel leaves the SIMDs idle at every barrier).  The block samples the tile's
+// frequencies plus a kSgPad halo on each side (clamped to the record; the last tile keeps at least
+// the 25 samples the right-edge fit reads), so the Savitzky-Golay pass of its outputs is local.
+// Only the FK columns the tile's frequencies touch are staged per image.
+constexpr int kTileThreads = 256;
+
+__global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
+    const double* __restrict__ FK, int32_t B, int32_t G, int32_t n_kb, int32_t n_fb,
+    const double* __restrict__ kgrid, double kmin, double kmax, const double* __restrict__ kq, int32_t nF,
+    int32_t nV, int32_t TO, const int32_t* __restrict__ fj, const double* __restrict__ fw,
+    const double* __restrict__ sg, int32_t sgl, float* __restrict__ fv) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int S = 2 * kSgPad + kTileThreads + 4;  // row stride (floats), multiple of 4
+  const int tid = threadIdx.x;
+  const int f_lo = blockIdx.x * TO, f_hi = min(nF, f_lo + TO);
+  const int half = sgl / 2;
+  const int s0 = max(0, f_lo - kSgPad);
+  const int s1 = min(nF, max(f_hi + kSgPad, sgl));
+  const int v0 = blockIdx.y * kFvVT;
+  __shared__ int jr[2];
+  if (tid == 0) {
+    jr[0] = 1 << 30;
+    jr[1] = -1;
+  }
+  __syncthreads();
+  const int f = s0 + tid;
+  const bool own = f < s1;
+  if (own) {
+    atomicMin(&jr[0], fj[f]);
+    atomicMax(&jr[1], fj[f]);
+  }
+  __syncthreads();
+  const int jlo = jr[0], ncol = jr[1] + 2 - jr[0];  // columns jlo .. jhi + 1
+  const int nsub = n_kb * ncol;
+  double* fks = smem;                                                 // [n_kb][ncol]
+  double* sgs = smem + ((n_kb * n_fb + 1) & ~1);                      // taps + edge fits
+  float* raw = reinterpret_cast<float*>(sgs + ((sgl * sgl + 1) & ~1));  // [kFvVT][S]
+  for (int e = tid; e < sgl * sgl; e += kTileThreads) sgs[e] = sg[e];
+  for (int e = tid; e < kFvVT * S; e += kTileThreads) raw[e] = 0.f;
+  const double* h = sgs;
+  const double* el = sgs + sgl;
+  const double* er = el + half * sgl;
+
+  int base[kFvVT];
+  double hx0[kFvVT], hx1[kFvVT], hy0 = 0.0, hy1 = 0.0;
+  {
+    const double k0 = kgrid[0], inv_dk = 1.0 / (kgrid[1] - kgrid[0]);
+    const int j = own ? fj[f] - jlo : 0;
+    if (own) {
+      hy0 = fw[2 * f];
+      hy1 = fw[2 * f + 1];
+    }
+#pragma unroll
+    for (int i = 0; i < kFvVT; ++i) {
+      const int v = v0 + i;
+      base[i] = -1;
+      hx0[i] = hx1[i] = 0.0;
+      if (own && v < nV) {
+        double q = kq[(int64_t)f * nV + v];
+        q = q < kmin ? kmin : (q > kmax ? kmax : q);
+        int m = (int)floor((q - k0) * inv_dk);
+        m = m < 0 ? 0 : (m > n_kb - 2 ? n_kb - 2 : m);
+        while (m < n_kb - 2 && q >= kgrid[m + 1]) ++m;
+        while (m > 0 && q < kgrid[m]) --m;
+        const double klo = kgrid[m], khi = kgrid[m + 1];
+        const double fx = 1.0 / (khi - klo);
+        hx0[i] = fx * (khi - q);
+        hx1[i] = fx * (q - klo);
+        base[i] = m * ncol + j;
+      }
+    }
+  }
+  const int nb4 = (f_hi - f_lo + 3) >> 2;
+  const bool fast_taps = (sgl == 2 * kSgPad + 1);
+  const int b0 = blockIdx.z * G;
+  const int n_img = min(G, B - b0);
+  for (int it = 0; it < n_img; ++it) {
+    const int b = b0 + it;
+    lds_barrier();  // the previous image is done with fks and raw
+    const double* F = FK + (int64_t)b * n_kb * n_fb + jlo;
+    for (int e = tid; e < nsub; e += kTileThreads) {
+      const int m = e / ncol, c = e - m * ncol;
+      fks[e] = F[m * n_fb + c];
+    }
+    lds_barrier();
+    if (own) {
+#pragma unroll
+      for (int i = 0; i < kFvVT; ++i) {
+        if (base[i] < 0) continue;
+        const int m = base[i];
+        const double z00 = fks[m], z01 = fks[m + 1], z10 = fks[m + ncol], z11 = fks[m + ncol + 1];
+        raw[i * S + kSgPad + tid] =
+            (float)(z00 * hx0[i] * hy0 + z01 * hx0[i] * hy1 + z10 * hx1[i] * hy0 + z11 * hx1[i] * hy1);
+      }
+    }
+    lds_barrier();
+    for (int task = tid; task < kFvVT * nb4; task += kTileThreads) {
+      const int r = task / nb4, f0 = f_lo + (task - r * nb4) * 4, v = v0 + r;
+      if (v >= nV) continue;
+      const float* row = raw + r * S + kSgPad - s0;  // row[x] = sample at frequency x
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      if (fast_taps && f0 >= half && f0 + 3 < nF - half && f0 + 3 < f_hi) {
+        float x[28];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+          const float4 t4 = *reinterpret_cast<const float4*>(row + f0 - kSgPad + 4 * q);
+          x[4 * q] = t4.x; x[4 * q + 1] = t4.y; x[4 * q + 2] = t4.z; x[4 * q + 3] = t4.w;
+        }
+#pragma unroll
+        for (int t = 0; t < 2 * kSgPad + 1; ++t) {
+          const double ht = sg[t];
+#pragma unroll
+          for (int o = 0; o < 4; ++o) acc[o] += ht * (double)x[o + t];
+        }
+      } else if (fast_taps) {  // edge (or partial) block, unrolled as in fv_batch_kernel
+        constexpr int L = 2 * kSgPad + 1;
+        const float* src = f0 < half ? row : row + nF - L;
+        float y[L];
+#pragma unroll
+        for (int t = 0; t < L; ++t) y[t] = src[t];
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          const int ff = f0 + o;
+          if (ff >= f_hi) break;
+          double a = 0.0;
+          if (ff < half || ff >= nF - half) {
+            const double* c = ff < half ? el + ff * L : er + (ff - (nF - half)) * L;
+#pragma unroll
+            for (int t = 0; t < L; ++t) a += c[t] * (double)y[t];
+          } else {
+#pragma unroll
+            for (int t = 0; t < L; ++t) a += sg[t] * (double)row[ff - half + t];
+          }
+          acc[o] = a;
+        }
+      } else {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          const int ff = f0 + o;
+          if (ff >= f_hi) break;
+          double a = 0.0;
+          if (ff < half) {
+            for (int t = 0; t < sgl; ++t) a += el[ff * sgl + t] * (double)row[t];
+          } else if (ff >= nF - half) {
+            const int rr = ff - (nF - half);
+            for (int t = 0; t < sgl; ++t) a += er[rr * sgl + t] * (double)row[nF - sgl + t];
+          } else {
+            for (int t = 0; t < sgl; ++t) a += h[t] * (double)row[ff - half + t];
+          }
+          acc[o] = a;
+        }
+      }
+      float* out = fv + ((int64_t)b * nV + v) * nF + f0;
+      if ((nF & 3) == 0 && f0 + 3 < f_hi) {
+        *reinterpret_cast<float4*>(out) = make_float4((float)acc[0], (float)acc[1], (float)acc[2], (float)acc[3]);
+      } else {
+#pragma unroll
+        for (int o = 0; o < 4; ++o)
+          if (f0 + o < f_hi) out[o] = (float)acc[o];
+      }
+    }
+  }
+}
+
 // per-row L1 norms -> 1 / ||row||_1 (map_fv norm=True: data / norm(data, ord=1, axis=-1))
 __global__ __launch_bounds__(256) void row_l1_kernel(const float* __restrict__ data, int64_t b_stride,
                                                       int64_t ch_stride, int32_t nch, int32_t nt,
@@ -489,6 +658,38 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
   if (sgl % 2 == 0 || sgl > nF) return set_error(-4, "savgol window must be odd and <= number of frequencies");
   if (B <= 0 || nV <= 0) return 0;
   // batched kernel: weights computed once per (f, v) and reused over G images of the block
+  // frequency-tiled kernel: tiles of TO outputs (multiple of 4, ~200), the last one >= kSgPad + 1
+  {
+    const int nt = (nF + 199) / 200;
+    int TO = (nF + nt - 1) / nt;
+    TO = (TO + 3) & ~3;
+    const int last = nF - (nt - 1) * TO;
+    int mode = DVH_FV_TILE;
+    if (const char* ev = getenv("DVH_FV_TILE")) mode = atoi(ev);  // A/B: 0 = batched / per-image, 2 = always tiled
+    const size_t lds_t = sizeof(double) * (size_t)(((size_t)n_kb * n_fb + 1) & ~(size_t)1) +
+                         sizeof(double) * (size_t)((sgl * sgl + 1) & ~1) +
+                         sizeof(float) * (size_t)kFvVT * (2 * kSgPad + kTileThreads + 4);
+    // large batches of long frequency axes only: on few images (the bench's 3 class stacks of
+    // 1 000 x 242) the per-image kernel measured faster (1.100 vs 1.125 ms per bench step), and with
+    // tiles under 160 outputs (nF = 242: 2 x 124) half the block idles -- the batched kernel packs
+    // 4 velocity groups there (sliding bench 16.2 vs 17.6 ms per step)
+    const int64_t work = (int64_t)B * nt * ((nV + kFvVT - 1) / kFvVT);
+    if (mode && ((work >= 8192 && TO >= 160) || mode > 1) && last >= kSgPad + 1 && TO + 2 * kSgPad <= kTileThreads &&
+        nF >= sgl && lds_t <= 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)fv_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds_t);
+      if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+      const int nvc = (nV + kFvVT - 1) / kFvVT;
+      const int64_t pairs = (int64_t)nt * nvc;
+      int G = (int)((pairs * B + 8191) / 8192);  // ~8 k blocks, at most 64 images each
+      G = G < 1 ? 1 : (G > 64 ? 64 : G);
+      if (const char* ev = getenv("DVH_FV_TG")) G = atoi(ev) > 0 ? atoi(ev) : G;
+      dim3 grid(nt, nvc, (B + G - 1) / G);
+      hipLaunchKernelGGL(fv_tile_kernel, grid, dim3(kTileThreads), lds_t, (hipStream_t)stream, FK, B, G, n_kb, n_fb,
+                         kgrid, kmin, kmax, kq, nF, nV, TO, fj, fw, sg, sgl, fv);
+      return last_launch();
+    }
+  }
   int n_grp = nF <= kFvThreads ? kFvThreads / nF : 0;
   n_grp = n_grp > 8 ? 8 : n_grp;
   if (!DVH_FV_LEGACY && n_grp > 0) {

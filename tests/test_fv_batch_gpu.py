@@ -9,12 +9,19 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 
-@pytest.mark.parametrize("G", [None, "3", "16"])
-@pytest.mark.parametrize("B,nv,nf", [(40, 512, 1000), (7, 300, 242), (5, 64, 1001)])
-def test_fv_batch_vs_oracle(device, monkeypatch, B, nv, nf, G):
-    """G: images per block of the batched kernel (DVH_FV_G, read at each launch); None = default dispatch."""
-    if G is not None:
-        monkeypatch.setenv("DVH_FV_G", G)
+@pytest.mark.parametrize("mode", [None, ("DVH_FV_TILE", "2"), ("DVH_FV_TILE", "0"), ("DVH_FV_G", "3"),
+                                  ("DVH_FV_G", "16"), ("DVH_FV_TG", "3"), ("DVH_FV_G", "0")])
+@pytest.mark.parametrize("B,nv,nf", [(40, 512, 1000), (7, 300, 242), (5, 64, 1001), (3, 61, 25), (4, 33, 413)])
+def test_fv_batch_vs_oracle(device, monkeypatch, B, nv, nf, mode):
+    """mode: kernel selection read at each launch -- None = default dispatch, DVH_FV_TILE=2 -> always
+    the frequency-tiled kernel, DVH_FV_TILE=0 -> batched / per-image dispatch, DVH_FV_G = images per block of the batched kernel (0: per-image
+    kernel), DVH_FV_TG = images per block of the tiled kernel."""
+    if mode is not None:
+        if mode[0] == "DVH_FV_G":
+            monkeypatch.setenv("DVH_FV_TILE", "0")
+        if mode[0] == "DVH_FV_TG":
+            monkeypatch.setenv("DVH_FV_TILE", "2")
+        monkeypatch.setenv(*mode)
     from das_diff_veh_amd.disp import DispPlan, fv_maps
     from das_diff_veh_amd.synth import synth_gathers
     from oracle import disp as odisp
