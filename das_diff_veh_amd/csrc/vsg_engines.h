@@ -540,6 +540,9 @@ struct Eng500 {
 #ifndef DVH_XB_ALWAYS
 #define DVH_XB_ALWAYS 0
 #endif
+#ifndef DVH_TW_REG
+#define DVH_TW_REG 0  // 1: per-lane twiddle powers held in registers (variant builds)
+#endif
 #ifndef DVH_DIAG_NOLOAD
 #define DVH_DIAG_NOLOAD 0
 #endif
@@ -559,12 +562,67 @@ struct EngF500 {
   float2* bufB;
   int lane;
   bool live_f, live_o;
+#if DVH_TW_REG
+  // this lane's twiddle powers of stages 2, 3 (two rounds each) and of its last-stage butterflies
+  // k = lane and 100 - lane, read once from the table: the lane -> butterfly map is the same for
+  // every transform of the wave, so the per-butterfly power recurrences disappear
+  float2 w2[2][4], w3[2][4], wA[4], wB[4];
+#endif
 
   __device__ EngF500(char* lds, int wave, int lane_) : lane(lane_), live_f(false), live_o(false) {
     tw = reinterpret_cast<float2*>(lds);
     bufA = reinterpret_cast<float2*>(lds + kBlockBytes + (size_t)wave * kWaveBytes);
     bufB = bufA + N;
+#if DVH_TW_REG
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = lane + 64 * r, k2 = i % 4, k3 = i % 20;
+#pragma unroll
+      for (int t = 1; t < 5; ++t) {
+        w2[r][t - 1] = tw[(t * k2 * 25) % N];
+        w3[r][t - 1] = tw[(t * k3 * 5) % N];
+      }
+    }
+    const int kb = (lane >= 1 && lane <= 49) ? 100 - lane : lane;
+#pragma unroll
+    for (int t = 1; t < 5; ++t) {
+      wA[t - 1] = tw[(t * lane) % N];
+      wB[t - 1] = tw[(t * kb) % N];
+    }
+#endif
   }
+
+#if DVH_TW_REG
+  // radix-5 Stockham stage of span Ls with this lane's register twiddles w[round][t - 1]
+  template <int Ls>
+  __device__ __forceinline__ void stage5(const float2* __restrict__ in, float2* __restrict__ out,
+                                         const float2 (&w)[2][4]) const {
+    constexpr int R = 5, NB = N / R;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = lane + 64 * r;
+      if (i < NB) {
+        const int k = i % Ls;
+        float2 a[R];
+#pragma unroll
+        for (int t = 0; t < R; ++t) a[t] = lds_ld(in, i + t * NB);
+#pragma unroll
+        for (int t = 1; t < R; ++t) a[t] = cmul(a[t], w[r][t - 1]);
+        Dft<R>::run(a);
+        const int base = (i - k) * R + k;
+#pragma unroll
+        for (int q = 0; q < R; ++q) out[base + q * Ls] = a[q];
+      }
+    }
+  }
+  __device__ __forceinline__ void last_bfly_reg(const float2* src, int k, const float2 (&w)[4], float2 (&x)[5]) const {
+#pragma unroll
+    for (int t = 0; t < 5; ++t) x[t] = lds_ld(src, k + 100 * t);
+#pragma unroll
+    for (int t = 1; t < 5; ++t) x[t] = cmul(x[t], w[t - 1]);
+    Dft<5>::run(x);
+  }
+#endif
   static __device__ void block_init(char* lds) { init_twiddles<N>(reinterpret_cast<float2*>(lds)); }
 
   static __device__ __forceinline__ int bin(int l, int j) {
@@ -613,6 +671,11 @@ struct EngF500 {
   template <class F>
   __device__ __forceinline__ void finish_with(F&& acc) const {
     wave_sync();
+#if DVH_TW_REG
+    stage5<4>(bufB, bufA, w2);
+    wave_sync();
+    stage5<20>(bufA, bufB, w3);
+#else
 #if DVH_DIAG_SKIP != 1  // timing diagnostics only (wrong results): 1 omits stage 2, 2 omits stage 3
     stockham_stage<N, 4, 5>(bufB, bufA, tw, lane);
     wave_sync();
@@ -620,15 +683,21 @@ struct EngF500 {
 #if DVH_DIAG_SKIP != 2
     stockham_stage<N, 20, 5>(bufA, bufB, tw, lane);
 #endif
+#endif
     wave_sync();
     if (lane <= 50) {
       float2 XA[5], XB[5];
-      last_bfly_from(bufB, lane, XA);
       const bool pair = lane >= 1 && lane <= 49;
+#if DVH_TW_REG
+      last_bfly_reg(bufB, lane, wA, XA);
+      if (pair) last_bfly_reg(bufB, 100 - lane, wB, XB);
+#else
+      last_bfly_from(bufB, lane, XA);
 #if DVH_XB_ALWAYS  // lanes 0 and 50 recompute their own butterfly: no branch between the two
       last_bfly_from(bufB, pair ? 100 - lane : lane, XB);
 #else
       if (pair) last_bfly_from(bufB, 100 - lane, XB);
+#endif
 #endif
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
