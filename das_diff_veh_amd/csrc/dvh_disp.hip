@@ -488,11 +488,25 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
   const bool fast_taps = (sgl == 2 * kSgPad + 1);
   const int b0 = blockIdx.z * G;
   const int n_img = min(G, B - b0);
+  // the sub-grid element -> FK offset map is the same for every image: computed once
+  constexpr int kStage = 3;  // elements per thread held as offsets (sub-grids up to 768 bins)
+  int goff[kStage];
+#pragma unroll
+  for (int q = 0; q < kStage; ++q) {
+    const int e = tid + q * kTileThreads;
+    const int m = e / ncol;
+    goff[q] = e < nsub ? m * n_fb + (e - m * ncol) : -1;
+  }
+  const int t_r = tid / nb4, t_f0 = f_lo + (tid - t_r * nb4) * 4;
+  const bool has_task = tid < kFvVT * nb4 && v0 + t_r < nV;
   for (int it = 0; it < n_img; ++it) {
     const int b = b0 + it;
     lds_barrier();  // the previous image is done with fks and raw
     const double* F = FK + (int64_t)b * n_kb * n_fb + jlo;
-    for (int e = tid; e < nsub; e += kTileThreads) {
+#pragma unroll
+    for (int q = 0; q < kStage; ++q)
+      if (goff[q] >= 0) fks[tid + q * kTileThreads] = F[goff[q]];
+    for (int e = tid + kStage * kTileThreads; e < nsub; e += kTileThreads) {
       const int m = e / ncol, c = e - m * ncol;
       fks[e] = F[m * n_fb + c];
     }
@@ -508,9 +522,9 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
       }
     }
     lds_barrier();
-    for (int task = tid; task < kFvVT * nb4; task += kTileThreads) {
-      const int r = task / nb4, f0 = f_lo + (task - r * nb4) * 4, v = v0 + r;
-      if (v >= nV) continue;
+    // one task per thread (4 nb4 <= kTileThreads: TO + 2 kSgPad <= kTileThreads)
+    if (has_task) {
+      const int r = t_r, f0 = t_f0, v = v0 + r;
       const float* row = raw + r * S + kSgPad - s0;  // row[x] = sample at frequency x
       double acc[4] = {0.0, 0.0, 0.0, 0.0};
       if (fast_taps && f0 >= half && f0 + 3 < nF - half && f0 + 3 < f_hi) {
