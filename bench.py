@@ -49,6 +49,9 @@ from das_diff_veh_amd.synth import TRACK_DT, synth_batch_device  # noqa: E402
 from das_diff_veh_amd.vsg import StackSchedule, vsg_scales, vsg_stack, window_sumsq  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 (non-packed) f32 VALU instruction every 4 cycles per SIMD
+# (16 lanes), at the 2,400 MHz max clock (MI355X_MICROARCH.md).  = 78.6 TFLOP/s of non-packed f32 FMA.
+VALU_PEAK_INSTR_S = 256 * 4 * 2.4e9 / 4
 
 WORKLOADS = {
     # name: (list of (pivot, start_x, end_x, class counts), n_ch, n_t, description, options)
@@ -327,6 +330,19 @@ def cpu_baseline(sets, budget_s=20.0, workers=None):
                 value_1core=rate1)
 
 
+def pmc_counter(kernel, workload, key):
+    """Per-launch value of `key` for `kernel` from the newest committed PMC summary of this workload."""
+    sfx = "" if workload == "weights" else "_" + workload
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_summary{sfx}.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in d and key in d[kernel]:
+            return float(d[kernel][key]), os.path.basename(f)
+    return None, None
+
+
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this
     workload (profiles/<round>_pmc_summary[_<workload>].json, written by tools/pmc.sh: FETCH_SIZE /
@@ -420,6 +436,13 @@ def main():
                      "launch_ms": launch_s * 1e3},
         "host_index_tables_s": sum(s.t_plan for s in sets),
     }
+    # companion roofline: the stack kernel is VALU-issue bound (DESIGN.md "Roofline of the stack kernel"),
+    # so report its VALU instructions per launch (PMC SQ_INSTS_VALU) / the live launch time vs the issue peak
+    valu, valu_src = pmc_counter("vsg_stackf_kernel", args.workload, "SQ_INSTS_VALU")
+    if valu is not None:
+        res["valu_roofline"] = {"achieved": valu / launch_s, "peak": VALU_PEAK_INSTR_S, "unit": "wave-instr/s",
+                                "frac": valu / launch_s / VALU_PEAK_INSTR_S, "instr_per_launch": valu,
+                                "source": valu_src, "clock_assumed_ghz": 2.4}
     res["config"]["gather_units_per_step_per_gpu"] = sum(s.units for s in sets)
     if any(s.host is None for s in sets):
         args.no_cpu_baseline = True  # the CPU loop images single-pivot windows (weights / speeds / synth10k)
