@@ -499,13 +499,21 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
   }
   const int t_r = tid / nb4, t_f0 = f_lo + (tid - t_r * nb4) * 4;
   const bool has_task = tid < kFvVT * nb4 && v0 + t_r < nV;
+  // the first kStage staged elements of image it + 1 are loaded into registers while image it is
+  // filtered, so the FK fetch latency is not exposed between barriers
+  double pre[kStage];
+  {
+    const double* F = FK + (int64_t)b0 * n_kb * n_fb + jlo;
+#pragma unroll
+    for (int q = 0; q < kStage; ++q) pre[q] = (n_img > 0 && goff[q] >= 0) ? F[goff[q]] : 0.0;
+  }
   for (int it = 0; it < n_img; ++it) {
     const int b = b0 + it;
     lds_barrier();  // the previous image is done with fks and raw
     const double* F = FK + (int64_t)b * n_kb * n_fb + jlo;
 #pragma unroll
     for (int q = 0; q < kStage; ++q)
-      if (goff[q] >= 0) fks[tid + q * kTileThreads] = F[goff[q]];
+      if (goff[q] >= 0) fks[tid + q * kTileThreads] = pre[q];
     for (int e = tid + kStage * kTileThreads; e < nsub; e += kTileThreads) {
       const int m = e / ncol, c = e - m * ncol;
       fks[e] = F[m * n_fb + c];
@@ -520,6 +528,12 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
         raw[i * S + kSgPad + tid] =
             (float)(z00 * hx0[i] * hy0 + z01 * hx0[i] * hy1 + z10 * hx1[i] * hy0 + z11 * hx1[i] * hy1);
       }
+    }
+    if (it + 1 < n_img) {
+      const double* Fn = F + (int64_t)n_kb * n_fb;
+#pragma unroll
+      for (int q = 0; q < kStage; ++q)
+        if (goff[q] >= 0) pre[q] = Fn[goff[q]];
     }
     lds_barrier();
     // one task per thread (4 nb4 <= kTileThreads: TO + 2 kSgPad <= kTileThreads)
