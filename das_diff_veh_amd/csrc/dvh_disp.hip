@@ -499,18 +499,13 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
   }
   const int t_r = tid / nb4, t_f0 = f_lo + (tid - t_r * nb4) * 4;
   const bool has_task = tid < kFvVT * nb4 && v0 + t_r < nV;
-  // the first kStage staged elements of image it + 1 are loaded into registers while image it is
-  // filtered, so the FK fetch latency is not exposed between barriers
+  // Two barriers per image: the next image's FK sub-grid is staged into fks while this image is
+  // filtered (fks is free once every thread has sampled), and its first kStage elements come from
+  // registers loaded one image earlier, so the FK fetch latency is not exposed between barriers.
+  const int64_t img_stride = (int64_t)n_kb * n_fb;
   double pre[kStage];
-  {
-    const double* F = FK + (int64_t)b0 * n_kb * n_fb + jlo;
-#pragma unroll
-    for (int q = 0; q < kStage; ++q) pre[q] = (n_img > 0 && goff[q] >= 0) ? F[goff[q]] : 0.0;
-  }
-  for (int it = 0; it < n_img; ++it) {
-    const int b = b0 + it;
-    lds_barrier();  // the previous image is done with fks and raw
-    const double* F = FK + (int64_t)b * n_kb * n_fb + jlo;
+  auto stage_img = [&](int it_s) {  // pre (image it_s) -> fks; the rest of the sub-grid from global
+    const double* F = FK + (int64_t)(b0 + it_s) * img_stride + jlo;
 #pragma unroll
     for (int q = 0; q < kStage; ++q)
       if (goff[q] >= 0) fks[tid + q * kTileThreads] = pre[q];
@@ -518,7 +513,21 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
       const int m = e / ncol, c = e - m * ncol;
       fks[e] = F[m * n_fb + c];
     }
-    lds_barrier();
+  };
+  auto load_pre = [&](int it_l) {
+    const double* F = FK + (int64_t)(b0 + it_l) * img_stride + jlo;
+#pragma unroll
+    for (int q = 0; q < kStage; ++q)
+      if (goff[q] >= 0) pre[q] = F[goff[q]];
+  };
+  if (n_img > 0) {
+    load_pre(0);
+    stage_img(0);
+    if (n_img > 1) load_pre(1);
+  }
+  for (int it = 0; it < n_img; ++it) {
+    const int b = b0 + it;
+    lds_barrier();  // fks holds image it; the previous image's filter is done with raw
     if (own) {
 #pragma unroll
       for (int i = 0; i < kFvVT; ++i) {
@@ -529,13 +538,11 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
             (float)(z00 * hx0[i] * hy0 + z01 * hx0[i] * hy1 + z10 * hx1[i] * hy0 + z11 * hx1[i] * hy1);
       }
     }
+    lds_barrier();  // raw holds image it; fks is free
     if (it + 1 < n_img) {
-      const double* Fn = F + (int64_t)n_kb * n_fb;
-#pragma unroll
-      for (int q = 0; q < kStage; ++q)
-        if (goff[q] >= 0) pre[q] = Fn[goff[q]];
+      stage_img(it + 1);
+      if (it + 2 < n_img) load_pre(it + 2);
     }
-    lds_barrier();
     // one task per thread (4 nb4 <= kTileThreads: TO + 2 kSgPad <= kTileThreads)
     if (has_task) {
       const int r = t_r, f0 = t_f0, v = v0 + r;
