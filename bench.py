@@ -232,11 +232,36 @@ def build(workload, device, world, rank, chunk=8):
     return out, desc
 
 
+def share_class_buffers(sets):
+    """Put every pivot's class stacks (and f-v images) in ONE HBM buffer when the pivots share the
+    gather geometry and the dispersion plan, so the step's f-v chain (tdft, FK contraction, f-v
+    sampling) runs once over all class images instead of once per pivot: those launches are
+    latency-bound at a few images each.  Returns (stack, fv, plan, rows) or None."""
+    s0 = sets[0]
+    if len(sets) < 2 or not all(hasattr(s, "disp_rows") for s in sets):
+        return None
+    p0 = s0.disp
+    for s in sets[1:]:
+        p = s.disp
+        if (s.disp_rows != s0.disp_rows or s.stack.shape[1:] != s0.stack.shape[1:]
+                or (p.nch, p.nt, p.dx, p.dt) != (p0.nch, p0.nt, p0.dx, p0.dt)
+                or not np.array_equal(p.freqs, p0.freqs) or not np.array_equal(p.vels, p0.vels)):
+            return None
+    n = [s.stack.shape[0] for s in sets]
+    stack = torch.zeros((sum(n),) + tuple(s0.stack.shape[1:]), dtype=s0.stack.dtype, device=s0.stack.device)
+    fv = torch.empty((sum(n),) + tuple(s0.fv.shape[1:]), dtype=s0.fv.dtype, device=s0.fv.device)
+    o = 0
+    for s, k in zip(sets, n):
+        s.stack, s.fv = stack[o:o + k], fv[o:o + k]
+        o += k
+    return stack, fv, p0, s0.disp_rows
+
+
 def launches(sets):
     return sum(len(s.batches) for s in sets)
 
 
-def step(sets, world, ev=None):
+def step(sets, world, ev=None, shared=None):
     k = 0
     for s in sets:
         for j, b in enumerate(s.batches):
@@ -248,7 +273,11 @@ def step(sets, world, ev=None):
                 ev[k][1].record()
             k += 1
     if world > 1:
-        allreduce_stacks([s.stack for s in sets])
+        allreduce_stacks([shared[0]] if shared is not None else [s.stack for s in sets])
+    if shared is not None:  # every pivot's class images in one f-v chain
+        stack, fv, plan, (a, b) = shared
+        fv_from_fk(fk_grid(stack[:, a:b, :], plan), plan, out=fv)
+        return
     for s in sets:
         a, b = s.disp_rows
         fv_from_fk(fk_grid(s.stack[:, a:b, :], s.disp), s.disp, out=s.fv)
@@ -366,6 +395,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="weights", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--per-pivot-fv", action="store_true", help="one f-v chain per pivot (no shared class buffer)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--chunk", type=int, default=8, help="passes per stack task (one wave, one gather row)")
     args = ap.parse_args()
@@ -385,8 +415,9 @@ def main():
         f"index tables in {sum(s.t_plan for s in sets):.2f}s; {sum(s.n_total for s in sets)} passes per step, "
         f"{launches(sets)} stack launches, R = {sets[0].plan.R}")
 
+    shared = None if args.per_pivot_fv else share_class_buffers(sets)
     for _ in range(args.warmup):
-        step(sets, world)
+        step(sets, world, shared=shared)
     torch.cuda.synchronize()
 
     ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(launches(sets))]
@@ -396,7 +427,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(sets, world, ev[k])
+        step(sets, world, ev[k], shared=shared)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

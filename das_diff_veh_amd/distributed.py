@@ -33,6 +33,9 @@ def allreduce_stacks(stacks, group=None):
     """In-place SUM of a list of same-dtype tensors across ranks with one bucketed collective."""
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return stacks
+    if len(stacks) == 1 and stacks[0].is_contiguous():  # one resident buffer: reduce in place
+        dist.all_reduce(stacks[0], op=dist.ReduceOp.SUM, group=group)
+        return stacks
     flat = torch.cat([t.reshape(-1) for t in stacks])
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     off = 0

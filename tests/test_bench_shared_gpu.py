@@ -1,0 +1,32 @@
+"""bench.py's shared class buffer: every pivot's class stacks in one HBM buffer and ONE f-v chain
+over all class images gives the per-pivot chains' images.  The stack kernel and the time-DFT add
+partials with atomics, so the last bits vary from run to run either way: the bound is 1e-5 of the
+image's peak, with identical picks per frequency column."""
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def test_shared_fv_chain_matches_per_pivot(device):
+    import bench
+    sets, _ = bench.build("weights", device, 1, 0, chunk=8)
+    bench.step(sets, 1)
+    torch.cuda.synchronize()
+    ref = [(s.stack.clone(), s.fv.clone()) for s in sets]
+    shared = bench.share_class_buffers(sets)
+    assert shared is not None and shared[0].shape[0] == sum(r[0].shape[0] for r in ref)
+    for _ in range(2):
+        shared[0].fill_(float("nan"))
+        shared[1].fill_(float("nan"))
+        bench.step(sets, 1, shared=shared)
+    torch.cuda.synchronize()
+    for (st, fv), s in zip(ref, sets):
+        for a, b in ((st, s.stack), (fv, s.fv)):
+            assert torch.isfinite(b).all()
+            assert ((a - b).abs().max() / a.abs().max()).item() < 1e-5
+        assert torch.equal(fv.argmax(dim=1), s.fv.argmax(dim=1))

@@ -31,6 +31,11 @@ def _worker(rank, world, port, q):
             part[slots[i]] += torch.from_numpy(x) / counts[slots[i]]
         extra = torch.full((3,), float(rank + 1), dtype=torch.float64)
         allreduce_stacks([part, extra])
+        one = torch.arange(6, dtype=torch.float64).reshape(2, 3) * (rank + 1)  # single buffer: in place
+        ptr = one.data_ptr()
+        allreduce_stacks([one])
+        assert one.data_ptr() == ptr
+        assert torch.equal(one, torch.arange(6, dtype=torch.float64).reshape(2, 3) * 3)
         q.put((rank, part.numpy(), extra.numpy(), mine.tolist()))
     finally:
         dist.destroy_process_group()
