@@ -128,6 +128,7 @@ class PivotSet:
             geoms = [pass_geometry(x_axis, t_axis, vx, vt, self.prm) for vx, vt in bt]
             plan = VsgPlan(geoms, self.prm, n_ch, n_t)
             self.batches.append(Batch(plan, StackSchedule(bs, len(counts), chunk=chunk, counts=global_counts)))
+            self.batches[-1].slots = bs
         self.plan = self.batches[0].plan
         self.t_plan = time.time() - t0
         self.gx, self.gt = geoms[0].gather_x_axis, geoms[0].gather_t_axis
@@ -255,6 +256,41 @@ def share_class_buffers(sets):
         s.stack, s.fv = stack[o:o + k], fv[o:o + k]
         o += k
     return stack, fv, p0, s0.disp_rows
+
+
+def merge_pivot_sets(sets, shared, chunk=8):
+    """One launch per step for every pivot's passes: the windows of all pivots in one resident
+    buffer and one index table (each pass carries its own pivot row), class slots numbered across
+    the pivots, so `vsg_scales` and `vsg_stack` run once over all passes instead of once per pivot
+    and the stacks land in the shared class buffer.  Returns a set-like object, or None when the
+    pivots do not share (rows, w, hop, flags) or are imaged in several batches."""
+    from types import SimpleNamespace
+    if shared is None or any(len(s.batches) != 1 or not hasattr(s.batches[0], "slots") for s in sets):
+        return None
+    if len({s.prm.flags for s in sets}) != 1:
+        return None
+    p0 = sets[0].batches[0].plan
+    try:
+        plan = VsgPlan([g for s in sets for g in s.batches[0].plan.geoms], sets[0].prm, p0.n_ch, p0.n_t)
+    except ValueError:
+        return None
+    win = torch.cat([s.windows for s in sets])
+    sumsq = torch.cat([s.sumsq for s in sets])
+    slots, counts, off, o = [], [], 0, 0
+    for s in sets:
+        b = s.batches[0]
+        slots.append(np.asarray(b.slots) + off)
+        counts.append(np.asarray(b.sched.counts))
+        off += b.sched.n_slot
+        n = s.windows.shape[0]
+        s.windows = b.win = win[o:o + n]  # the per-pivot views share the merged buffer
+        s.sumsq = b.sumsq = sumsq[o:o + n]
+        o += n
+    sched = StackSchedule(np.concatenate(slots), off, chunk=chunk, counts=np.concatenate(counts))
+    batch = Batch(plan, sched, win=win, sumsq=sumsq,
+                  scales=torch.empty((plan.n_pass, 2), dtype=torch.float32, device=win.device))
+    return SimpleNamespace(batches=[batch], stack=shared[0], fv=shared[1], disp=shared[2], disp_rows=shared[3],
+                           plan=plan, bytes_stack=[plan.algorithmic_bytes(out_rows=off * plan.R)])
 
 
 def launches(sets):
@@ -395,6 +431,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="weights", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--per-pivot-launch", action="store_true", help="one scales + stack launch per pivot")
     ap.add_argument("--per-pivot-fv", action="store_true", help="one f-v chain per pivot (no shared class buffer)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--chunk", type=int, default=8, help="passes per stack task (one wave, one gather row)")
@@ -416,18 +453,20 @@ def main():
         f"{launches(sets)} stack launches, R = {sets[0].plan.R}")
 
     shared = None if args.per_pivot_fv else share_class_buffers(sets)
+    merged = None if args.per_pivot_launch else merge_pivot_sets(sets, shared, chunk=args.chunk)
+    run = [merged] if merged is not None else sets  # what one step launches
     for _ in range(args.warmup):
-        step(sets, world, shared=shared)
+        step(run, world, shared=shared)
     torch.cuda.synchronize()
 
-    ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(launches(sets))]
+    ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(launches(run))]
           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(sets, world, ev[k], shared=shared)
+        step(run, world, ev[k], shared=shared)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -435,12 +474,12 @@ def main():
     if world > 1:
         elapsed = max_over_ranks(elapsed, device)
 
-    stack_ms = np.array([[ev[k][i][0].elapsed_time(ev[k][i][1]) for i in range(launches(sets))]
+    stack_ms = np.array([[ev[k][i][0].elapsed_time(ev[k][i][1]) for i in range(launches(run))]
                          for k in range(args.steps)])
     windows_per_step = sum(s.n_total for s in sets) * world
     images_per_step = sum(s.stack.shape[0] for s in sets)
     # roofline of the dominant kernel (vsg_stack): algorithmic bytes per launch / mean launch time
-    bytes_per_launch = float(np.mean([b for s in sets for b in s.bytes_stack]))
+    bytes_per_launch = float(np.mean([b for s in run for b in s.bytes_stack]))
     launch_s = float(stack_ms.mean()) / 1e3
     achieved = bytes_per_launch / launch_s / 1e9
     traffic, traffic_src = pmc_traffic("vsg_stackf_kernel", args.workload)
@@ -475,6 +514,7 @@ def main():
                                 "frac": valu / launch_s / VALU_PEAK_INSTR_S, "instr_per_launch": valu,
                                 "source": valu_src, "clock_assumed_ghz": 2.4}
     res["config"]["gather_units_per_step_per_gpu"] = sum(s.units for s in sets)
+    res["config"]["stack_launches_per_step"] = launches(run)
     if any(s.host is None for s in sets):
         args.no_cpu_baseline = True  # the CPU loop images single-pivot windows (weights / speeds / synth10k)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -30,3 +30,27 @@ def test_shared_fv_chain_matches_per_pivot(device):
             assert torch.isfinite(b).all()
             assert ((a - b).abs().max() / a.abs().max()).item() < 1e-5
         assert torch.equal(fv.argmax(dim=1), s.fv.argmax(dim=1))
+
+
+def test_merged_launch_matches_per_pivot(device):
+    """Both pivots' passes in ONE scales + stack launch (merged index table, slots numbered across
+    the pivots) give the per-pivot launches' class stacks and images."""
+    import bench
+    sets, _ = bench.build("weights", device, 1, 0, chunk=8)
+    bench.step(sets, 1)
+    torch.cuda.synchronize()
+    ref = [(s.stack.clone(), s.fv.clone()) for s in sets]
+    shared = bench.share_class_buffers(sets)
+    merged = bench.merge_pivot_sets(sets, shared, chunk=8)
+    assert merged is not None
+    assert merged.plan.n_pass == sum(s.n_total for s in sets)
+    for _ in range(2):
+        shared[0].fill_(float("nan"))
+        shared[1].fill_(float("nan"))
+        bench.step([merged], 1, shared=shared)
+    torch.cuda.synchronize()
+    for (st, fv), s in zip(ref, sets):
+        for a, b in ((st, s.stack), (fv, s.fv)):
+            assert torch.isfinite(b).all()
+            assert ((a - b).abs().max() / a.abs().max()).item() < 1e-5
+        assert torch.equal(fv.argmax(dim=1), s.fv.argmax(dim=1))
