@@ -512,7 +512,10 @@ def main():
     if valu is not None:
         res["valu_roofline"] = {"achieved": valu / launch_s, "peak": VALU_PEAK_INSTR_S, "unit": "wave-instr/s",
                                 "frac": valu / launch_s / VALU_PEAK_INSTR_S, "instr_per_launch": valu,
-                                "source": valu_src, "clock_assumed_ghz": 2.4}
+                                "source": valu_src, "clock_assumed_ghz": 2.4,
+                                "model": "every wave64 VALU instruction 4 cycles on its SIMD at the 2.4 GHz max clock; "
+                                         "frac near or above 1 = VALU-issue bound (some instructions, e.g. moves "
+                                         "and packed ops, issue in fewer cycles than the model charges)"}
     res["config"]["gather_units_per_step_per_gpu"] = sum(s.units for s in sets)
     res["config"]["stack_launches_per_step"] = launches(run)
     if any(s.host is None for s in sets):
