@@ -1,27 +1,32 @@
 #!/usr/bin/env python
 """Throughput bench of the vehicle-pass imaging hot path on MI355X (one process per GPU).
 
-Workload (default = BASELINE.json configs[1], "700_weights + 680_weights"): two synthetic window
-sets, one per pivot (700 m and 680 m), each 1,895 vehicle passes of 60 channels x 5,500 samples
-(8.16 m, dt = 0.004 s), split into heavy / mid / light classes of 103 / 1,058 / 734 passes
-(imaging_diff_weight.ipynb#cell8).  One step = for every pivot: the per-pass amplitude scales,
-the two-sided VSG of every pass fused with the per-class stack (sum / len), [multi-GPU: one
-all-reduce of the partial class stacks], then the f-v image of every class stack
-(compute_disp_image(end_x=0, start_x=-200): 1,000 velocities x 242 frequencies).
-Inputs are resident in HBM before the timed region; the host-side index tables are built once.
+Default workload = BASELINE.json configs[2], "synth10k", the largest single-GPU configuration:
+10,240 synthetic vehicle passes of 1,024 channels x 8,192 samples (8.16 m, dt = 0.004 s), one pivot
+(channel 512), every channel a gather row (R = 1,023), speed-tercile classes.  The job's 335 GB of
+fp32 windows exceed HBM, so a pool of 512 windows is resident and one step images the 10,240 passes
+as 20 batches over that pool, each batch with its own 512 trajectories (window contents repeat across
+batches, the per-pass work does not).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload weights|speeds|synth10k|sliding]
+One step, per batch, all on the device and on one stream:
+  1. the batch's index tables from its trajectories      dvh_pass_geometry   (preprocessing_window)
+  2. the windows' validity ||window||_F^2                 dvh_window_sumsq    (data / ||data||_F)
+  3. the per-pass amplitude scales                        dvh_vsg_scales      (post_processing_XCF)
+  4. the two-sided VSG of every pass fused with the class stack     dvh_vsg_stack
+then [N > 1: one all-reduce of the partial class stacks] and the f-v image of every class stack
+(compute_disp_image(end_x=0, start_x=-200): 1,000 velocities x 242 frequencies).  Only the windows
+and the trajectories are resident before the timed region.
 
-synth10k (BASELINE.json configs[2]): 10,240 passes x 1,024 channels x 8,192 samples, single pivot
-at channel 512, all channels in the gather aperture, speed-tercile classes.  The job (335 GB of
-fp32 windows) exceeds HBM, so a pool of 512 passes is resident and a step images the 10,240 passes
-as 20 batches over that pool, each batch with its own 512 per-pass trajectories (index tables);
-window contents repeat across batches, the per-pass work does not.
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload synth10k|weights|speeds|sliding]
+                    [--scaling weak|strong]
 
-sliding (BASELINE.json configs[3]): 4,096-channel x 8,192-sample windows imaged at sliding pivots
-(every 8 channels, +-200 m) -- one unit per (pass, pivot crossed inside the window), slots = speed
-class x pivot, one f-v image per slot (SlidingSet).  12,544 passes per GPU per step (100k over 8
-GPUs), 49 batches over a resident pool of 256 windows (34 GB).
+weak (default): every rank images its own full job (value = N x the job per step).  strong: ONE job
+of the configured size is split over the ranks (das_diff_veh_amd.distributed.shard_passes: every
+class dealt round robin), class means with the global counts, one all-reduce.
+weights (configs[1]): two pivots (700 m, 680 m) x 1,895 passes (heavy/mid/light 103/1,058/734) of
+60 x 5,500 in ONE resident buffer, one launch of each kernel per step, 6 class images.
+sliding (configs[3]): 4,096-channel windows imaged at every pivot they cross (host O(C + J) unit
+tables, validity of the resident pool computed at ingest), see DESIGN.md.
 
 Prints ONE JSON line (rank 0).  `value` = vehicle-pass windows per second over all ranks.
 """
@@ -43,32 +48,37 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from das_diff_veh_amd.disp import DispPlan, fk_grid, fv_from_fk  # noqa: E402
-from das_diff_veh_amd.distributed import allreduce_stacks, max_over_ranks  # noqa: E402
-from das_diff_veh_amd.plan import VsgParams, VsgPlan, pass_geometry  # noqa: E402
+from das_diff_veh_amd.distributed import allreduce_stacks, max_over_ranks, shard_passes  # noqa: E402
+from das_diff_veh_amd.plan import DevicePlan, VsgParams  # noqa: E402
 from das_diff_veh_amd.synth import TRACK_DT, synth_batch_device  # noqa: E402
 from das_diff_veh_amd.vsg import StackSchedule, vsg_scales, vsg_stack, window_sumsq  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 (non-packed) f32 VALU instruction every 4 cycles per SIMD
-# (16 lanes), at the 2,400 MHz max clock (MI355X_MICROARCH.md).  = 78.6 TFLOP/s of non-packed f32 FMA.
-VALU_PEAK_INSTR_S = 256 * 4 * 2.4e9 / 4
+# VALU issue peak: 256 CUs x 4 SIMD-32s, one wave64 VALU instruction per 2 cycles per SIMD once >= 2
+# waves share the SIMD (MI355X_MICROARCH.md "Wave scheduling" and the v_fma_f32 row of the cycle
+# constants), at the 2,400 MHz max clock = 1.229 T wave-instructions/s.
+VALU_PEAK_INSTR_S = 256 * 4 * 2.4e9 / 2
 
 WORKLOADS = {
-    # name: (list of (pivot, start_x, end_x, class counts), n_ch, n_t, description, options)
-    "weights": ([(700.0, 500.0, 900.0, (103, 1058, 734)), (680.0, 480.0, 880.0, (103, 1058, 734))], 60, 5500,
-                "configs[1]: 700_weights + 680_weights, heavy/mid/light 103/1058/734 per pivot, 60ch x 5500", {}),
-    "speeds": ([(700.0, 500.0, 900.0, (330, 1442, 336))], 60, 5500,
-               "configs[0]-shape: 700_speeds, fast/mid/slow 330/1442/336, 60ch x 5500", {}),
-    "sliding": ([(None, None, None, 12544)], 4096, 8192,
-                "configs[3]: synthetic passes x 4096ch x 8192, sliding pivots every 8 channels (+-200 m, 49 rows), "
-                "each pass imaged at every pivot it crosses inside its window; 12,544 passes per GPU (100k over 8) "
-                "as 49 batches over a resident pool of 256 passes; speed classes x pivots stacked, f-v image per "
-                "(class, pivot)",
-                dict(sliding=True, pool=256, pivot_every=8, half_aperture=200.0, gen_chunk=2)),
-    "synth10k": ([(4178.0, 0.0, 8400.0, 10240)], 1024, 8192,
-                 "configs[2]: synthetic 10,240 passes x 1024ch x 8192, pivot = channel 512, all channels, "
-                 "speed-tercile classes; 20 batches over a resident pool of 512 passes",
-                 dict(pool=512, x_first=0.37, track_half=4300, gen_chunk=8)),
+    "synth10k": dict(kind="pool", config="configs[2]", pivot=(4178.0, 0.0, 8400.0), n_total=10240, n_ch=1024, n_t=8192,
+                     pool=512, x_first=0.37, gen_chunk=8, track_half=4300,
+                     desc="configs[2]: synthetic 10,240 passes x 1024 ch x 8192, pivot = channel 512, all channels "
+                          "(R = 1023), speed-tercile classes; 20 batches of 512 over a resident window pool, each "
+                          "batch with its own trajectories"),
+    "weights": dict(kind="resident", config="configs[1]",
+                    pivots=[(700.0, 500.0, 900.0, (103, 1058, 734)), (680.0, 480.0, 880.0, (103, 1058, 734))],
+                    n_ch=60, n_t=5500, gen_chunk=64, track_half=350,
+                    desc="configs[1]: 700_weights + 680_weights, heavy/mid/light 103/1058/734 per pivot, 60 ch x 5500, "
+                         "both pivots in one launch"),
+    "speeds": dict(kind="resident", config="configs[0]-shape", pivots=[(700.0, 500.0, 900.0, (330, 1442, 336))],
+                   n_ch=60, n_t=5500, gen_chunk=64, track_half=350,
+                   desc="configs[0]-shape: 700_speeds, fast/mid/slow 330/1442/336, 60 ch x 5500"),
+    "sliding": dict(kind="sliding", config="configs[3]", n_total=12544, n_ch=4096, n_t=8192, pool=256, pivot_every=8,
+                    half_aperture=200.0, gen_chunk=2,
+                    desc="configs[3]: synthetic passes x 4096 ch x 8192, sliding pivots every 8 channels (+-200 m, "
+                         "49 rows), each pass imaged at every pivot it crosses inside its window; 12,544 passes per "
+                         "GPU (100k over 8) as 49 batches over a resident pool of 256 windows; speed classes x "
+                         "pivots stacked, f-v image per (class, pivot)"),
 }
 
 
@@ -77,256 +87,260 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def tercile_slots(speeds):
+    """Exact speed terciles (equal-as-possible class sizes)."""
+    slots = np.empty(speeds.size, dtype=np.int64)
+    slots[np.argsort(speeds, kind="stable")] = np.arange(speeds.size) * 3 // speeds.size
+    return slots
+
+
 class Batch:
-    """One launch's worth of passes: their index tables and class schedule over the resident windows
-    (``win`` / ``sumsq``: the launch view of the windows and its per-pass ||window||_F^2)."""
+    """One launch's worth of passes: the device plan (tables derived in the step), the class
+    schedule, the launch view of the windows and its validity / scale buffers."""
 
-    def __init__(self, plan, sched, win=None, sumsq=None, scales=None):
-        self.plan, self.sched = plan, sched
-        self.win, self.sumsq, self.scales = win, sumsq, scales
-
-
-class PivotSet:
-    """One window set imaged at one pivot: device windows, index tables, class schedule.
-
-    ``counts`` is either the per-class pass counts (all passes resident) or, with options["pool"],
-    the total number of passes, imaged in batches of `pool` resident windows (speed-tercile classes)."""
-
-    def __init__(self, pivot, start_x, end_x, counts, n_ch, n_t, seed, device, world, rank, opts, chunk=8):
-        pool = opts.get("pool")
-        n = pool or int(sum(counts))
-        self.n = n
-        t0 = time.time()
-        self.windows, x_axis, t_axis, trk, _ = synth_batch_device(
-            n, n_ch=n_ch, n_t=n_t, pivot=pivot, seed=seed, device=device, x_first=opts.get("x_first"),
-            track_half=opts.get("track_half", 350), chunk=opts.get("gen_chunk", 64))
-        self.t_gen = time.time() - t0
-        t0 = time.time()
-        self.prm = VsgParams(pivot=pivot, start_x=start_x, end_x=end_x, wlen=2, norm=False, include_other_side=True)
-        rng = np.random.default_rng(seed + 7)
-        if pool:
-            n_total = int(counts)
-            n_batch = -(-n_total // pool)
-            xs_trk = trk[0][0]
-            speeds = rng.uniform(15.0, 30.0, n_batch * pool)
-            tcs = t_axis[n_t // 2] + rng.uniform(-1.0, 1.0, n_batch * pool)
-            # speed terciles by rank (exact, equal-as-possible counts: every rank has the same class
-            # sizes, so the global counts are world x the local ones)
-            slots_all = np.empty(speeds.size, dtype=np.int64)
-            slots_all[np.argsort(speeds, kind="stable")] = np.arange(speeds.size) * 3 // speeds.size
-            counts = np.bincount(slots_all, minlength=3)
-            trks = [(xs_trk, np.round((tc + (xs_trk - pivot) / v) / TRACK_DT) * TRACK_DT) for v, tc in zip(speeds, tcs)]
-            batch_trk = [trks[b * pool:(b + 1) * pool] for b in range(n_batch)]
-            batch_slots = [slots_all[b * pool:(b + 1) * pool] for b in range(n_batch)]
-        else:
-            batch_trk = [trk]
-            batch_slots = [rng.permutation(np.repeat(np.arange(len(counts)), counts))]
-        self.n_total = sum(len(t) for t in batch_trk)
-        global_counts = np.asarray(counts) * world  # every rank holds its own full set (weak scaling)
-        self.batches = []
-        for bt, bs in zip(batch_trk, batch_slots):
-            geoms = [pass_geometry(x_axis, t_axis, vx, vt, self.prm) for vx, vt in bt]
-            plan = VsgPlan(geoms, self.prm, n_ch, n_t)
-            self.batches.append(Batch(plan, StackSchedule(bs, len(counts), chunk=chunk, counts=global_counts)))
-            self.batches[-1].slots = bs
-        self.plan = self.batches[0].plan
-        self.t_plan = time.time() - t0
-        self.gx, self.gt = geoms[0].gather_x_axis, geoms[0].gather_t_axis
-        self.stack = torch.zeros((len(counts), self.plan.R, self.plan.w), dtype=torch.float32, device=device)
-        self.scales = torch.empty((n, 2), dtype=torch.float32, device=device)
-        # ||window||_F^2 is a property of the resident windows (validity: finite, not all zero ->
-        # the reference's data / ||data||_F), computed once at ingest like the index tables
-        self.sumsq = window_sumsq(self.windows)
-        s = int(np.abs(self.gx - (-200.0)).argmin())
-        e = int(np.abs(self.gx - 0.0).argmin())
-        self.disp_rows = (s, e + 1)
-        self.disp = DispPlan(e + 1 - s, self.plan.w, 8.16, self.gt[1] - self.gt[0], np.arange(0.8, 25, 0.1),
-                             np.arange(200, 1200))
-        self.fv = torch.empty((len(counts), self.disp.nV, self.disp.nF), dtype=torch.float32, device=device)
-        self.bytes_stack = [b.plan.algorithmic_bytes(out_rows=len(counts) * self.plan.R) for b in self.batches]
-        self.host = (x_axis, t_axis, batch_trk[0])
-        for b in self.batches:
-            b.win, b.sumsq, b.scales = self.windows, self.sumsq, self.scales
-        self.units = self.n_total
+    def __init__(self, plan, sched, win, sumsq, scales, derive=True, validity=True):
+        self.plan, self.sched, self.win, self.sumsq, self.scales = plan, sched, win, sumsq, scales
+        self.derive, self.validity = derive, validity
 
 
-class SlidingSet:
-    """BASELINE configs[3]: a pool of long-fiber windows imaged at sliding pivots (UnitPlan).
+class Job:
+    """Everything one rank launches per step: batches, class stacks, the f-v chain."""
 
-    Every batch gives the pool new per-pass trajectories (crossing point uniform along the fiber,
-    15-30 m/s, crossing at mid-window); a pass becomes one unit per pivot it crosses inside its
-    window (all rows with full-length slices on both sides).  Slots = speed class x pivot with
-    fixed class edges (20, 25 m/s), so that every rank's slots mean the same thing; the class means
-    use the GLOBAL unit count per slot (one all-reduce of the counts at setup)."""
-
-    def __init__(self, n_total, n_ch, n_t, seed, device, world, rank, opts, chunk=8):
-        from das_diff_veh_amd.plan import UnitPlan, sliding_pivots
-        from das_diff_veh_amd.vsg import flat_units, unit_sumsq
-        pool = opts["pool"]
-        self.n = pool
-        t0 = time.time()
-        self.windows, x_axis, t_axis, _, _ = synth_batch_device(
-            pool, n_ch=n_ch, n_t=n_t, pivot=n_ch * 8.16 / 2, seed=seed, device=device, x_first=0.37,
-            track_half=10, chunk=opts.get("gen_chunk", 2))
-        self.t_gen = time.time() - t0
-        t0 = time.time()
-        self.prm = VsgParams(wlen=2, norm=False, include_other_side=True)
-        edge = 4 * opts["pivot_every"]
-        pch = np.arange(edge, n_ch - edge, opts["pivot_every"])
-        n_piv = pch.size
-        rng = np.random.default_rng(seed + 7)
-        n_batch = -(-int(n_total) // pool)
-        self.n_total = n_batch * pool
-        sumsq = window_sumsq(self.windows)
-        plans, slot_l = [], []
-        for _ in range(n_batch):
-            x0 = rng.uniform(x_axis[edge], x_axis[-edge], pool)
-            v = rng.uniform(15.0, 30.0, pool)
-            tc = t_axis[n_t // 2] + rng.uniform(-1.0, 1.0, pool)
-            trk = []
-            for xa, va, ta in zip(x0, v, tc):
-                xs = np.arange(np.floor(xa) - 800.0, np.floor(xa) + 801.0)
-                trk.append((xs, np.round((ta + (xs - xa) / va) / TRACK_DT) * TRACK_DT))
-            plan = UnitPlan.sliding(x_axis, t_axis, trk, pch, opts["half_aperture"], self.prm)
-            cls = np.digitize(v[plan.unit_window], [20.0, 25.0])
-            plans.append(plan)
-            slot_l.append(cls * n_piv + plan.unit_pivot)
-        n_slot = 3 * n_piv
-        counts = np.bincount(np.concatenate(slot_l), minlength=n_slot)
-        if world > 1:
-            ct = torch.as_tensor(counts, dtype=torch.int64, device=device)
-            dist.all_reduce(ct)
-            counts = ct.cpu().numpy()
-        self.batches = []
-        for plan, sl in zip(plans, slot_l):
-            b = Batch(plan, StackSchedule(sl, n_slot, chunk=chunk, counts=counts), win=flat_units(self.windows, plan),
-                      sumsq=unit_sumsq(sumsq, plan),
-                      scales=torch.empty((plan.n_pass, 2), dtype=torch.float32, device=device))
-            self.batches.append(b)
-        self.units = sum(p.n_pass for p in plans)
-        self.plan = plans[0]
-        self.t_plan = time.time() - t0
-        R, w = self.plan.R, self.plan.w
-        dt = t_axis[1] - t_axis[0]
-        pv, st, en, _ = sliding_pivots(x_axis, pch[:1], opts["half_aperture"])
-        self.gx = x_axis[st[0]:en[0]] - x_axis[pv[0]]
-        self.gt = (np.arange(w) - w // 2) * dt
+    def finish(self, n_slot, R, w, gx, dt, device):
         self.stack = torch.zeros((n_slot, R, w), dtype=torch.float32, device=device)
-        s = int(np.abs(self.gx - (-200.0)).argmin())
-        e = int(np.abs(self.gx - 0.0).argmin())
+        s = int(np.abs(gx - (-200.0)).argmin())
+        e = int(np.abs(gx - 0.0).argmin())
         self.disp_rows = (s, e + 1)
         self.disp = DispPlan(e + 1 - s, w, 8.16, dt, np.arange(0.8, 25, 0.1), np.arange(200, 1200))
         self.fv = torch.empty((n_slot, self.disp.nV, self.disp.nF), dtype=torch.float32, device=device)
-        self.bytes_stack = [p.algorithmic_bytes(out_rows=n_slot * R) for p in plans]
-        self.host = None
 
 
-def build(workload, device, world, rank, chunk=8):
-    sets, n_ch, n_t, desc, opts = WORKLOADS[workload]
-    out = []
-    if opts.get("sliding"):
-        return [SlidingSet(sets[0][3], n_ch, n_t, seed=1000 * rank + 3, device=device, world=world, rank=rank,
-                           opts=opts, chunk=chunk)], desc
-    for i, (pivot, sx, ex, counts) in enumerate(sets):
-        out.append(PivotSet(pivot, sx, ex, counts, n_ch, n_t, seed=1000 * rank + 17 * i + 3, device=device,
-                            world=world, rank=rank, opts=opts, chunk=chunk))
-    return out, desc
+def build_pool(wl, device, world, rank, scaling, chunk):
+    """configs[2]: a resident pool of windows, batches of `pool` passes with their own trajectories."""
+    job = Job()
+    pivot, start_x, end_x = wl["pivot"]
+    n_ch, n_t, pool = wl["n_ch"], wl["n_t"], wl["pool"]
+    t0 = time.time()
+    job.windows, x_axis, t_axis, _, _ = synth_batch_device(pool, n_ch=n_ch, n_t=n_t, pivot=pivot, seed=1000 * rank + 3,
+                                                           device=device, x_first=wl["x_first"], track_half=10,
+                                                           chunk=wl["gen_chunk"])
+    job.t_gen = time.time() - t0
+    # the job's passes: speeds 15-30 m/s, pivot crossing within +-1 s of mid-window, on the 1 m / 50 Hz
+    # tracking grid.  weak: each rank its own job (seeded by rank); strong: one global job, sharded.
+    seed = 7 if scaling == "strong" else 1000 * rank + 7
+    rng = np.random.default_rng(seed)
+    n_job = wl["n_total"]
+    speeds = rng.uniform(15.0, 30.0, n_job)
+    tcs = t_axis[n_t // 2] + rng.uniform(-1.0, 1.0, n_job)
+    slots = tercile_slots(speeds)
+    if scaling == "strong":
+        mine = shard_passes(slots, world, rank)
+        counts = np.bincount(slots, minlength=3)
+    else:
+        mine = np.arange(n_job)
+        counts = np.bincount(slots, minlength=3) * world  # every rank has the same class sizes
+    xs = np.arange(np.floor(pivot) - wl["track_half"], np.floor(pivot) + wl["track_half"] + 1, 1.0)
+    t0 = time.time()
+    prm = VsgParams(pivot=pivot, start_x=start_x, end_x=end_x, wlen=2, norm=False, include_other_side=True)
+    n_loc = mine.size
+    trk_t = torch.empty((n_loc, xs.size), dtype=torch.float64, device=device)
+    for b in range(0, n_loc, 1024):  # trajectories to the device in slices (bounded host memory)
+        idx = mine[b:b + 1024]
+        tt = np.round((tcs[idx, None] + (xs[None, :] - pivot) / speeds[idx, None]) / TRACK_DT) * TRACK_DT
+        trk_t[b:b + idx.size].copy_(torch.from_numpy(tt))
+    trk_x = torch.from_numpy(xs).to(device).expand(n_loc, xs.size).contiguous()
+    trk_len = torch.full((n_loc,), xs.size, dtype=torch.int32, device=device)
+    job.sumsq = torch.empty(pool, dtype=torch.float64, device=device)
+    job.scales = torch.empty((pool, 2), dtype=torch.float32, device=device)
+    seg_buf = None
+    job.batches = []
+    for b in range(0, n_loc, pool):
+        sl = slice(b, min(b + pool, n_loc))
+        nb = sl.stop - sl.start
+        plan = DevicePlan(x_axis, t_axis, trk_x[sl], trk_t[sl], trk_len[sl], prm, n_ch, derive=False,
+                          seg_out=seg_buf)
+        seg_buf = plan.seg_tab if seg_buf is None else seg_buf  # one table buffer for every batch
+        sched = StackSchedule(slots[mine[sl]], 3, chunk=chunk, counts=counts)
+        job.batches.append(Batch(plan, sched, job.windows[:nb], job.sumsq[:nb], job.scales[:nb]))
+        job.batches[-1].slots = slots[mine[sl]]
+    job.t_plan = time.time() - t0
+    job.n_local, job.n_global = n_loc, (n_job if scaling == "strong" else n_job * world)
+    job.units = n_loc
+    job.prm, job.x_axis, job.t_axis = prm, x_axis, t_axis
+    # host copies of a few passes for the CPU baseline (the reference loop takes host arrays)
+    job.cpu_sets = [dict(win=job.windows, x_axis=x_axis, t_axis=t_axis, prm=prm, n_total=job.n_global,
+                         trk=[(xs, np.round((tcs[i] + (xs - pivot) / speeds[i]) / TRACK_DT) * TRACK_DT) for i in mine[:64]])]
+    R, w = job.batches[0].plan.R, job.batches[0].plan.w
+    st, pv = int(np.argmax(x_axis >= start_x)), int(np.argmax(x_axis >= pivot))
+    job.finish(3, R, w, x_axis[st:st + R] - x_axis[pv], t_axis[1] - t_axis[0], device)
+    return job
 
 
-def share_class_buffers(sets):
-    """Put every pivot's class stacks (and f-v images) in ONE HBM buffer when the pivots share the
-    gather geometry and the dispersion plan, so the step's f-v chain (tdft, FK contraction, f-v
-    sampling) runs once over all class images instead of once per pivot: those launches are
-    latency-bound at a few images each.  Returns (stack, fv, plan, rows) or None."""
-    s0 = sets[0]
-    if len(sets) < 2 or not all(hasattr(s, "disp_rows") for s in sets):
-        return None
-    p0 = s0.disp
-    for s in sets[1:]:
-        p = s.disp
-        if (s.disp_rows != s0.disp_rows or s.stack.shape[1:] != s0.stack.shape[1:]
-                or (p.nch, p.nt, p.dx, p.dt) != (p0.nch, p0.nt, p0.dx, p0.dt)
-                or not np.array_equal(p.freqs, p0.freqs) or not np.array_equal(p.vels, p0.vels)):
-            return None
-    n = [s.stack.shape[0] for s in sets]
-    stack = torch.zeros((sum(n),) + tuple(s0.stack.shape[1:]), dtype=s0.stack.dtype, device=s0.stack.device)
-    fv = torch.empty((sum(n),) + tuple(s0.fv.shape[1:]), dtype=s0.fv.dtype, device=s0.fv.device)
+def build_resident(wl, device, world, rank, scaling, chunk):
+    """configs[0]/[1]: every pass of every pivot set resident in ONE window buffer, one launch."""
+    job = Job()
+    n_ch, n_t = wl["n_ch"], wl["n_t"]
+    sets = wl["pivots"]
+    # the job: per pivot set its class labels (seeded identically on every rank for strong scaling)
+    slots_g, set_g = [], []
+    for i, (_, _, _, counts) in enumerate(sets):
+        rng = np.random.default_rng(100 + i if scaling == "strong" else 1000 * rank + 100 + i)
+        slots_g.append(rng.permutation(np.repeat(np.arange(len(counts)), counts)) + 3 * i)
+        set_g.append(np.full(int(sum(counts)), i))
+    slots_g, set_g = np.concatenate(slots_g), np.concatenate(set_g)
+    n_slot = 3 * len(sets)
+    if scaling == "strong":
+        mine = shard_passes(slots_g, world, rank)
+        counts = np.bincount(slots_g, minlength=n_slot)
+    else:
+        mine = np.arange(slots_g.size)
+        counts = np.bincount(slots_g, minlength=n_slot) * world
+    n = mine.size
+    job.windows = torch.empty((n, n_ch, n_t), dtype=torch.float32, device=device)
+    t0 = time.time()
+    x_axes = np.empty((n, n_ch))
+    trks, piv, sx, ex, job.cpu_sets = [], np.empty(n), np.empty(n), np.empty(n), []
     o = 0
-    for s, k in zip(sets, n):
-        s.stack, s.fv = stack[o:o + k], fv[o:o + k]
+    for i, (pivot, start_x, end_x, _) in enumerate(sets):
+        k = int(np.sum(set_g[mine] == i))
+        if k == 0:
+            continue
+        _, x_axis, t_axis, trk, _ = synth_batch_device(k, n_ch=n_ch, n_t=n_t, pivot=pivot, seed=1000 * rank + 17 * i + 3,
+                                                       device=device, track_half=wl["track_half"],
+                                                       chunk=wl["gen_chunk"], out=job.windows[o:o + k])
+        x_axes[o:o + k], piv[o:o + k], sx[o:o + k], ex[o:o + k] = x_axis, pivot, start_x, end_x
+        trks += trk
+        job.cpu_sets.append(dict(win=job.windows[o:o + k], x_axis=x_axis, t_axis=t_axis, trk=trk[:64],
+                                 prm=VsgParams(pivot=pivot, start_x=start_x, end_x=end_x, wlen=2, norm=False,
+                                               include_other_side=True),
+                                 n_total=int(np.sum(set_g == i)) * (1 if scaling == "strong" else world)))
         o += k
-    return stack, fv, p0, s0.disp_rows
+    job.t_gen = time.time() - t0
+    t0 = time.time()
+    slots_l = slots_g[mine]  # `mine` is ascending and set-major: buffer order
+    from das_diff_veh_amd.plan import pack_trajectories
+    prm = job.cpu_sets[0]["prm"]
+    plan = DevicePlan(x_axes, t_axis, *pack_trajectories(trks, device), prm, n_ch, pivot_x=piv, start_x=sx, end_x=ex,
+                      derive=False)
+    sched = StackSchedule(slots_l, n_slot, chunk=chunk, counts=counts)
+    job.sumsq = torch.empty(n, dtype=torch.float64, device=device)
+    job.scales = torch.empty((n, 2), dtype=torch.float32, device=device)
+    job.batches = [Batch(plan, sched, job.windows, job.sumsq, job.scales)]
+    job.batches[0].slots = slots_l
+    job.t_plan = time.time() - t0
+    job.n_local = n
+    job.n_global = slots_g.size if scaling == "strong" else slots_g.size * world
+    job.units = n
+    pv0 = int(np.argmax(x_axes[0] >= piv[0]))
+    st0 = int(np.argmax(x_axes[0] >= sx[0]))
+    job.finish(n_slot, plan.R, plan.w, x_axes[0, st0:st0 + plan.R] - x_axes[0, pv0], t_axis[1] - t_axis[0], device)
+    return job
 
 
-def merge_pivot_sets(sets, shared, chunk=8):
-    """One launch per step for every pivot's passes: the windows of all pivots in one resident
-    buffer and one index table (each pass carries its own pivot row), class slots numbered across
-    the pivots, so `vsg_scales` and `vsg_stack` run once over all passes instead of once per pivot
-    and the stacks land in the shared class buffer.  Returns a set-like object, or None when the
-    pivots do not share (rows, w, hop, flags) or are imaged in several batches."""
-    from types import SimpleNamespace
-    if shared is None or any(len(s.batches) != 1 or not hasattr(s.batches[0], "slots") for s in sets):
-        return None
-    if len({s.prm.flags for s in sets}) != 1:
-        return None
-    p0 = sets[0].batches[0].plan
-    try:
-        plan = VsgPlan([g for s in sets for g in s.batches[0].plan.geoms], sets[0].prm, p0.n_ch, p0.n_t)
-    except ValueError:
-        return None
-    win = torch.cat([s.windows for s in sets])
-    sumsq = torch.cat([s.sumsq for s in sets])
-    slots, counts, off, o = [], [], 0, 0
-    for s in sets:
-        b = s.batches[0]
-        slots.append(np.asarray(b.slots) + off)
-        counts.append(np.asarray(b.sched.counts))
-        off += b.sched.n_slot
-        n = s.windows.shape[0]
-        s.windows = b.win = win[o:o + n]  # the per-pivot views share the merged buffer
-        s.sumsq = b.sumsq = sumsq[o:o + n]
-        o += n
-    sched = StackSchedule(np.concatenate(slots), off, chunk=chunk, counts=np.concatenate(counts))
-    batch = Batch(plan, sched, win=win, sumsq=sumsq,
-                  scales=torch.empty((plan.n_pass, 2), dtype=torch.float32, device=win.device))
-    return SimpleNamespace(batches=[batch], stack=shared[0], fv=shared[1], disp=shared[2], disp_rows=shared[3],
-                           plan=plan, bytes_stack=[plan.algorithmic_bytes(out_rows=off * plan.R)])
+def build_sliding(wl, device, world, rank, scaling, chunk):
+    """configs[3]: a pool of long-fiber windows imaged at sliding pivots (UnitPlan, host tables).
 
-
-def launches(sets):
-    return sum(len(s.batches) for s in sets)
-
-
-def step(sets, world, ev=None, shared=None):
-    k = 0
-    for s in sets:
-        for j, b in enumerate(s.batches):
-            vsg_scales(b.win, b.plan, out=b.scales, win_sumsq=b.sumsq)
-            if ev is not None:
-                ev[k][0].record()
-            vsg_stack(b.win, b.plan, b.sched, scales=b.scales, out=s.stack, accumulate=j > 0)
-            if ev is not None:
-                ev[k][1].record()
-            k += 1
+    Every batch gives the pool new per-pass trajectories (crossing point uniform along the fiber,
+    15-30 m/s, crossing at mid-window); a pass becomes one unit per pivot it crosses inside its
+    window.  Slots = speed class x pivot with fixed class edges (20, 25 m/s); class means use the
+    GLOBAL unit count per slot (one all-reduce of the counts at setup).  The pool's validity is
+    computed once at ingest (its windows are resident for the whole run)."""
+    from das_diff_veh_amd.plan import UnitPlan, sliding_pivots
+    from das_diff_veh_amd.vsg import flat_units, unit_sumsq
+    job = Job()
+    n_ch, n_t, pool = wl["n_ch"], wl["n_t"], wl["pool"]
+    t0 = time.time()
+    job.windows, x_axis, t_axis, _, _ = synth_batch_device(pool, n_ch=n_ch, n_t=n_t, pivot=n_ch * 8.16 / 2,
+                                                           seed=1000 * rank + 3, device=device, x_first=0.37,
+                                                           track_half=10, chunk=wl["gen_chunk"])
+    job.t_gen = time.time() - t0
+    t0 = time.time()
+    prm = VsgParams(wlen=2, norm=False, include_other_side=True)
+    edge = 4 * wl["pivot_every"]
+    pch = np.arange(edge, n_ch - edge, wl["pivot_every"])
+    n_piv = pch.size
+    n_total = wl["n_total"] if scaling == "weak" else -(-wl["n_total"] // world)
+    rng = np.random.default_rng(1000 * rank + 7)
+    n_batch = -(-int(n_total) // pool)
+    sumsq = window_sumsq(job.windows)
+    plans, slot_l = [], []
+    for _ in range(n_batch):
+        x0 = rng.uniform(x_axis[edge], x_axis[-edge], pool)
+        v = rng.uniform(15.0, 30.0, pool)
+        tc = t_axis[n_t // 2] + rng.uniform(-1.0, 1.0, pool)
+        trk = []
+        for xa, va, ta in zip(x0, v, tc):
+            xs = np.arange(np.floor(xa) - 800.0, np.floor(xa) + 801.0)
+            trk.append((xs, np.round((ta + (xs - xa) / va) / TRACK_DT) * TRACK_DT))
+        plan = UnitPlan.sliding(x_axis, t_axis, trk, pch, wl["half_aperture"], prm)
+        plans.append(plan)
+        slot_l.append(np.digitize(v[plan.unit_window], [20.0, 25.0]) * n_piv + plan.unit_pivot)
+    n_slot = 3 * n_piv
+    counts = np.bincount(np.concatenate(slot_l), minlength=n_slot)
     if world > 1:
-        allreduce_stacks([shared[0]] if shared is not None else [s.stack for s in sets])
-    if shared is not None:  # every pivot's class images in one f-v chain
-        stack, fv, plan, (a, b) = shared
-        fv_from_fk(fk_grid(stack[:, a:b, :], plan), plan, out=fv)
-        return
-    for s in sets:
-        a, b = s.disp_rows
-        fv_from_fk(fk_grid(s.stack[:, a:b, :], s.disp), s.disp, out=s.fv)
+        ct = torch.as_tensor(counts, dtype=torch.int64, device=device)
+        dist.all_reduce(ct)
+        counts = ct.cpu().numpy()
+    job.batches = []
+    for plan, sl in zip(plans, slot_l):
+        job.batches.append(Batch(plan, StackSchedule(sl, n_slot, chunk=chunk, counts=counts),
+                                 flat_units(job.windows, plan), unit_sumsq(sumsq, plan),
+                                 torch.empty((plan.n_pass, 2), dtype=torch.float32, device=device),
+                                 derive=False, validity=False))
+    job.units = sum(p.n_pass for p in plans)
+    job.n_local = n_batch * pool
+    job.n_global = job.n_local * world
+    job.t_plan = time.time() - t0
+    job.cpu_sets = None
+    R, w = plans[0].R, plans[0].w
+    pv, st, en, _ = sliding_pivots(x_axis, pch[:1], wl["half_aperture"])
+    job.finish(n_slot, R, w, x_axis[st[0]:en[0]] - x_axis[pv[0]], t_axis[1] - t_axis[0], device)
+    return job
 
 
-def cpu_baseline(sets, budget_s=20.0, workers=None):
+def build(workload, device, world, rank, scaling="weak", chunk=8):
+    wl = WORKLOADS[workload]
+    fn = {"pool": build_pool, "resident": build_resident, "sliding": build_sliding}[wl["kind"]]
+    return fn(wl, device, world, rank, scaling, chunk)
+
+
+PHASES = ("geometry", "validity", "scales", "stack")
+
+
+def step(job, world, ev=None):
+    """One step; ev (optional) = {phase: list of [start, end] events, one pair per batch}."""
+    def mark(name, j, k):
+        if ev is not None:
+            ev[name][j][k].record()
+    for j, b in enumerate(job.batches):
+        mark("geometry", j, 0)
+        if b.derive:
+            b.plan.derive()
+        mark("geometry", j, 1)
+        mark("validity", j, 0)
+        if b.validity:
+            window_sumsq(b.win, out=b.sumsq)
+        mark("validity", j, 1)
+        mark("scales", j, 0)
+        vsg_scales(b.win, b.plan, out=b.scales, win_sumsq=b.sumsq)
+        mark("scales", j, 1)
+        mark("stack", j, 0)
+        vsg_stack(b.win, b.plan, b.sched, scales=b.scales, out=job.stack, accumulate=j > 0)
+        mark("stack", j, 1)
+    if world > 1:
+        allreduce_stacks([job.stack])
+    a, e = job.disp_rows
+    fv_from_fk(fk_grid(job.stack[:, a:e, :], job.disp), job.disp, out=job.fv)
+
+
+def cpu_baseline(job, budget_s=20.0, workers=None):
     """Reference-structured CPU path (oracle/ref_loop.py) on a bounded sample of the same windows.
 
     1 core: the bench windows themselves (host copies) for about budget_s / 2, plus one f-v image
-    per set.  All cores: `workers` single-threaded processes (spawned, no GPU state; the box's CPU
-    share is 16) each looping over a saved sample of the windows for budget_s / 2; the value is the
-    aggregate windows/s, extrapolated with the 1-core image cost to one full step."""
-    import multiprocessing as mp
+    per pivot set.  All cores: `workers` single-threaded processes (spawned, no GPU state; the box's
+    CPU share is 16) each looping over a saved sample of the windows for budget_s / 2; the value is
+    the aggregate windows/s, extrapolated with the 1-core image cost to one full step."""
+    import subprocess
     import tempfile
 
     from oracle import ref_loop
@@ -335,36 +349,35 @@ def cpu_baseline(sets, budget_s=20.0, workers=None):
     n_win, t_win, t_img, n_img = 0, 0.0, 0.0, 0
     t_start = time.time()
     one_budget = budget_s / 2
-    per_set = max(4, int(one_budget / 0.01 / max(len(sets), 1)))
     samples = []
-    for s in sets:
-        x_axis, t_axis, trk = s.host
-        k = min(per_set, s.n, max(4, int(2e9 / (8 * s.windows[0].numel()))))  # host copy <= 2 GB
-        host = s.windows[:k].to("cpu", torch.float64).numpy()
-        samples.append((host[:16].astype(np.float32), x_axis, t_axis, trk[:16], s.prm))
+    for s in job.cpu_sets:
+        x_axis, t_axis, trk, prm, win = s["x_axis"], s["t_axis"], s["trk"], s["prm"], s["win"]
+        wbytes = 8 * win[0].numel()
+        k = min(len(trk), win.shape[0], max(2, int(2e9 / wbytes)))  # host copy <= 2 GB
+        host = win[:k].to("cpu", torch.float64).numpy()
+        ns = max(2, min(16, k, int(256e6 / (wbytes / 2))))  # worker sample <= 256 MB of float32
+        samples.append((host[:ns].astype(np.float32), x_axis, t_axis, trk[:ns], prm))
         t0 = time.time()
         acc = None
+        done = 0
         for i in range(k):
-            g, gx, gt = ref_loop.gather(host[i], x_axis, t_axis, trk[i][0], trk[i][1], s.prm.pivot, s.prm.start_x,
-                                        s.prm.end_x)
+            g, gx, gt = ref_loop.gather(host[i], x_axis, t_axis, trk[i][0], trk[i][1], prm.pivot, prm.start_x,
+                                        prm.end_x)
             acc = g if acc is None else acc + g
+            done += 1
             if time.time() - t_start > one_budget:
-                k = i + 1
                 break
         t_win += time.time() - t0
-        n_win += k
+        n_win += done
         t0 = time.time()
-        ref_loop.disp_image(acc / k, gx, gt)
+        ref_loop.disp_image(acc / done, gx, gt)
         t_img += time.time() - t0
         n_img += 1
     per_window = t_win / n_win
     per_image = t_img / n_img
-    total_windows = sum(s.n_total for s in sets)
-    total_images = sum(s.stack.shape[0] for s in sets)
+    total_windows = sum(s["n_total"] for s in job.cpu_sets)
+    total_images = job.stack.shape[0]
     rate1 = total_windows / (per_window * total_windows + per_image * total_images)
-    # all cores: single-threaded worker processes (plain python, no torch / GPU state) over a saved
-    # sample of the first set's windows, all running at once
-    import subprocess
     host, x_axis, t_axis, trk, prm = samples[0]
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     with tempfile.TemporaryDirectory() as d:
@@ -377,7 +390,7 @@ def cpu_baseline(sets, budget_s=20.0, workers=None):
         res = []
         for pr in procs:
             try:
-                out, _ = pr.communicate(timeout=budget_s * 4 + 60)
+                out, _ = pr.communicate(timeout=budget_s * 4 + 120)
                 done, secs = out.split()
                 res.append((int(done), float(secs)))
             except Exception:  # a worker that failed or hung does not count
@@ -388,53 +401,49 @@ def cpu_baseline(sets, budget_s=20.0, workers=None):
     agg_window_rate = sum(n / t for n, t in res)
     step_s = total_windows / agg_window_rate + per_image * total_images / workers
     return dict(value=total_windows / step_s, unit="vehicle-pass windows/s", cores=workers, kind="port",
-                sample=f"all cores: {workers} single-threaded processes x {budget_s / 2:.0f} s, {sum(n for n, _ in res)} "
-                       f"windows (VSG two-sided), f-v images at the 1-core cost / {workers}; 1 core: {n_win} windows "
-                       f"({per_window * 1e3:.1f} ms/window), {n_img} f-v images ({per_image * 1e3:.1f} ms/image) -> "
-                       f"{rate1:.1f} windows/s; cpu={platform.processor() or platform.machine()}",
+                sample=f"all cores: {workers} single-threaded processes x {budget_s / 2:.0f} s over {host.shape[0]} "
+                       f"saved windows, {sum(n for n, _ in res)} windows (VSG two-sided), f-v images at the 1-core "
+                       f"cost / {workers}; 1 core: {n_win} windows ({per_window * 1e3:.1f} ms/window), {n_img} f-v "
+                       f"images ({per_image * 1e3:.1f} ms/image) -> {rate1:.2f} windows/s; "
+                       f"cpu={platform.processor() or platform.machine()}",
                 value_1core=rate1)
 
 
-def pmc_counter(kernel, workload, key):
-    """Per-launch value of `key` for `kernel` from the newest committed PMC summary of this workload."""
-    sfx = "" if workload == "weights" else "_" + workload
+def layout_of(job, args):
+    """What one profiled launch of the stack kernel covers (PMC counters are per launch)."""
+    return {"workload": args.workload, "chunk": args.chunk, "scaling": args.scaling,
+            "passes_per_launch": [int(b.plan.n_pass) for b in job.batches][:1],
+            "launches_per_step": len(job.batches)}
+
+
+def pmc_lookup(kernel, layout, key):
+    """Per-launch value of `key` for `kernel` from the newest committed PMC summary whose recorded
+    launch layout equals this run's.  (None, note) when no summary matches: counters of a different
+    launch shape divided by this run's launch time would be wrong by the ratio of the shapes."""
+    sfx = "" if layout["workload"] == "synth10k" else "_" + layout["workload"]
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_summary{sfx}.json")), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
+            continue
+        if d.get("layout") != layout:
             continue
         if kernel in d and key in d[kernel]:
             return float(d[kernel][key]), os.path.basename(f)
-    return None, None
-
-
-def pmc_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this
-    workload (profiles/<round>_pmc_summary[_<workload>].json, written by tools/pmc.sh: FETCH_SIZE /
-    WRITE_SIZE with the access-width calibration measured by tools/calib/fetch_calib).  (None, None)
-    if absent."""
-    sfx = "" if workload == "weights" else "_" + workload
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_summary{sfx}.json")), reverse=True):
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
-            continue
-        if kernel in d and "traffic_bytes" in d[kernel]:
-            return float(d[kernel]["traffic_bytes"]), os.path.basename(f)
-    return None, None
+    return None, "no committed PMC summary with this launch layout"
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="weights", choices=sorted(WORKLOADS))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="synth10k", choices=sorted(WORKLOADS))
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--per-pivot-launch", action="store_true", help="one scales + stack launch per pivot")
-    ap.add_argument("--per-pivot-fv", action="store_true", help="one f-v chain per pivot (no shared class buffer)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--chunk", type=int, default=8, help="passes per stack task (one wave, one gather row)")
+    ap.add_argument("--layout-out", default=None, help="write the launch layout (JSON) for tools/pmc_summary.py")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -446,27 +455,37 @@ def main():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         dist.init_process_group("nccl", device_id=device)
 
-    sets, desc = build(args.workload, device, world, rank, chunk=args.chunk)
+    job = build(args.workload, device, world, rank, args.scaling, chunk=args.chunk)
     torch.cuda.synchronize()
-    log(f"[bench] rank {rank}: generated {sum(s.n for s in sets)} windows in {sum(s.t_gen for s in sets):.2f}s, "
-        f"index tables in {sum(s.t_plan for s in sets):.2f}s; {sum(s.n_total for s in sets)} passes per step, "
-        f"{launches(sets)} stack launches, R = {sets[0].plan.R}")
+    log(f"[bench] rank {rank}: {job.windows.shape[0]} resident windows generated in {job.t_gen:.2f}s, host setup "
+        f"{job.t_plan:.2f}s; {job.n_local} passes per step on this rank ({job.units} units), "
+        f"{len(job.batches)} batches, R = {job.batches[0].plan.R}")
+    if args.layout_out and rank == 0:
+        with open(args.layout_out, "w") as fh:
+            json.dump(layout_of(job, args), fh)
 
-    shared = None if args.per_pivot_fv else share_class_buffers(sets)
-    merged = None if args.per_pivot_launch else merge_pivot_sets(sets, shared, chunk=args.chunk)
-    run = [merged] if merged is not None else sets  # what one step launches
     for _ in range(args.warmup):
-        step(run, world, shared=shared)
+        step(job, world)
+    torch.cuda.synchronize()
+    # algorithmic bytes of every stack launch (bookkeeping outside the timed region: the tables of
+    # the last derived batch are on the device; re-derive each and copy it back once)
+    bytes_stack = []
+    for b in job.batches:
+        if b.derive:
+            b.plan.derive()
+        bytes_stack.append(b.plan.algorithmic_bytes(out_rows=job.stack.shape[0] * job.stack.shape[1]))
+    win_bytes = [4 * b.win.shape[0] * b.win.shape[1] * b.win.shape[2] if b.validity else 0 for b in job.batches]
     torch.cuda.synchronize()
 
-    ev = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(launches(run))]
-          for _ in range(args.steps)]
+    nb = len(job.batches)
+    ev = [{p: [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(nb)]
+           for p in PHASES} for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(run, world, ev[k], shared=shared)
+        step(job, world, ev[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -474,15 +493,17 @@ def main():
     if world > 1:
         elapsed = max_over_ranks(elapsed, device)
 
-    stack_ms = np.array([[ev[k][i][0].elapsed_time(ev[k][i][1]) for i in range(launches(run))]
-                         for k in range(args.steps)])
-    windows_per_step = sum(s.n_total for s in sets) * world
-    images_per_step = sum(s.stack.shape[0] for s in sets)
+    ms = {p: np.array([[ev[k][p][j][0].elapsed_time(ev[k][p][j][1]) for j in range(nb)] for k in range(args.steps)])
+          for p in PHASES}
+    windows_per_step = job.n_global
+    images_per_step = job.stack.shape[0]
     # roofline of the dominant kernel (vsg_stack): algorithmic bytes per launch / mean launch time
-    bytes_per_launch = float(np.mean([b for s in run for b in s.bytes_stack]))
-    launch_s = float(stack_ms.mean()) / 1e3
+    bytes_per_launch = float(np.mean(bytes_stack))
+    launch_s = float(ms["stack"].mean()) / 1e3
     achieved = bytes_per_launch / launch_s / 1e9
-    traffic, traffic_src = pmc_traffic("vsg_stackf_kernel", args.workload)
+    layout = layout_of(job, args)
+    traffic, traffic_src = pmc_lookup("vsg_stackf_kernel", layout, "traffic_bytes")
+    step_ms = elapsed / args.steps * 1e3
     res = {
         "metric": "vehicle-pass windows/sec -> stacked VSG + f-v images/sec; % HBM/MFMA roofline",
         "value": windows_per_step * args.steps / elapsed,
@@ -490,38 +511,40 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": step_ms,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (device-generated dispersive moving-source wavefield, per-pass trajectories)",
-        "config": {"workload": args.workload, "description": desc, "windows_per_step_per_gpu": windows_per_step // world,
-                   "class_images_per_step": images_per_step, "gather_rows": sets[0].plan.R, "w": sets[0].plan.w,
-                   "parallelism": f"dp{world} (passes sharded, all-reduce of class stacks)", "chunk": args.chunk},
+        "config": {"workload": args.workload, "baseline_config": WORKLOADS[args.workload]["config"],
+                   "description": WORKLOADS[args.workload]["desc"],
+                   "windows_per_step": windows_per_step, "windows_per_step_this_rank": job.n_local,
+                   "class_images_per_step": images_per_step, "gather_rows": job.batches[0].plan.R,
+                   "w": job.batches[0].plan.w, "parallelism": f"dp{world} (passes sharded, all-reduce of class stacks)",
+                   "chunk": args.chunk, "gather_units_per_step_this_rank": job.units, "stack_launches_per_step": nb},
         "images_per_s": images_per_step * args.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "vsg_stackf_kernel", "bytes_per_launch": bytes_per_launch,
                      "launch_ms": launch_s * 1e3},
-        "host_index_tables_s": sum(s.t_plan for s in sets),
+        "step_breakdown_ms": {p: float(ms[p].sum(axis=1).mean()) for p in PHASES},
+        "host_setup_s": job.t_plan,
     }
-    # companion roofline: the stack kernel is VALU-issue bound (DESIGN.md "Roofline of the stack kernel"),
-    # so report its VALU instructions per launch (PMC SQ_INSTS_VALU) / the live launch time vs the issue peak
-    valu, valu_src = pmc_counter("vsg_stackf_kernel", args.workload, "SQ_INSTS_VALU")
-    if valu is not None:
-        res["valu_roofline"] = {"achieved": valu / launch_s, "peak": VALU_PEAK_INSTR_S, "unit": "wave-instr/s",
-                                "frac": valu / launch_s / VALU_PEAK_INSTR_S, "instr_per_launch": valu,
-                                "source": valu_src, "clock_assumed_ghz": 2.4,
-                                "model": "every wave64 VALU instruction 4 cycles on its SIMD at the 2.4 GHz max clock; "
-                                         "frac near or above 1 = VALU-issue bound (some instructions, e.g. moves "
-                                         "and packed ops, issue in fewer cycles than the model charges)"}
-    res["config"]["gather_units_per_step_per_gpu"] = sum(s.units for s in sets)
-    res["config"]["stack_launches_per_step"] = launches(run)
-    if any(s.host is None for s in sets):
-        args.no_cpu_baseline = True  # the CPU loop images single-pivot windows (weights / speeds / synth10k)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(sets, args.cpu_budget)
+    res["step_breakdown_ms"]["fv_allreduce_rest"] = step_ms - sum(res["step_breakdown_ms"].values())
+    if any(win_bytes):
+        vs = float(ms["validity"].mean()) / 1e3
+        res["validity_roofline"] = {"kernel": "window_sumsq_kernel", "bytes_per_launch": float(np.mean(win_bytes)),
+                                    "launch_ms": vs * 1e3, "achieved": float(np.mean(win_bytes)) / vs / 1e9,
+                                    "frac": float(np.mean(win_bytes)) / vs / 1e9 / HBM_PEAK_GBS}
+    valu, valu_src = pmc_lookup("vsg_stackf_kernel", layout, "SQ_INSTS_VALU")
+    res["valu_roofline"] = {"achieved": None if valu is None else valu / launch_s, "peak": VALU_PEAK_INSTR_S,
+                            "unit": "wave-instr/s", "frac": None if valu is None else valu / launch_s / VALU_PEAK_INSTR_S,
+                            "instr_per_launch": valu, "source": valu_src, "clock_assumed_ghz": 2.4,
+                            "model": "wave64 VALU instruction = 2 cycles on a SIMD-32 (>= 2 waves per SIMD) at the "
+                                     "2.4 GHz max clock"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and job.cpu_sets:
+        cb = cpu_baseline(job, args.cpu_budget)
         res["cpu_baseline"] = cb
         res["speedup_vs_cpu"] = res["value"] / cb["value"]
     else:

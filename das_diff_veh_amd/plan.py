@@ -58,6 +58,56 @@ def py_slice(a, b, n):
     return a, np.maximum(b - a, 0)
 
 
+def seg_nwin(seg_tab, w, hop):
+    """Sub-windows per (pass, row, side): (L - w) // hop + 1, or 0 when the slice is shorter than w."""
+    L = np.asarray(seg_tab)[..., 1].astype(np.int64)
+    return np.where(L >= w, (L - w) // hop + 1, 0)
+
+
+def seg_algorithmic_bytes(seg_tab, w, hop, sides, out_rows=0):
+    """Bytes a launch must move for the tables seg_tab [n, R, 2, 2]: 4 B x every receiver sample under
+    a sub-window, 4 B x each distinct pivot sample of a pass (the union of its rows' slices), and
+    out_rows gather rows of w fp32 written."""
+    seg = np.asarray(seg_tab)
+    n = seg.shape[0]
+    nw = seg_nwin(seg, w, hop)[:, :, :sides]
+    cov = np.where(nw > 0, (nw - 1) * hop + w, 0).astype(np.int64)
+    rcv = 4 * int(cov.sum())
+    # union of the pivot-channel intervals [a, a + cov) per pass: sort by start, running max of ends
+    a = seg[:, :, :sides, 0].reshape(n, -1).astype(np.int64)
+    e = a + cov.reshape(n, -1)
+    o = np.argsort(a, axis=1, kind="stable")
+    a, e = np.take_along_axis(a, o, 1), np.take_along_axis(e, o, 1)
+    prev = np.concatenate([np.full((n, 1), np.iinfo(np.int64).min), np.maximum.accumulate(e, axis=1)[:, :-1]], 1)
+    piv = 4 * int(np.maximum(e - np.maximum(a, prev), 0).sum())
+    return rcv + piv + 4 * out_rows * w
+
+
+def spatial_indices(x_axis, pivot, start_x, end_x):
+    """(pivot_idx, start_idx, end_idx) of preprocessing_window (apis/virtual_shot_gather.py:111-126):
+    argmax(x >= pivot), argmax(x >= start_x), argmin |x - end_x|; x_axis [C] with scalars, or [n, C]
+    with scalars or per-pass [n] values."""
+    x = np.asarray(x_axis, dtype=np.float64)
+    if x.ndim == 1:
+        return (int(np.argmax(x >= pivot)), int(np.argmax(x >= start_x)), int(np.abs(x - end_x).argmin()))
+    col = lambda v: np.asarray(v, dtype=np.float64).reshape(-1, 1)  # noqa: E731
+    return (np.argmax(x >= col(pivot), axis=1), np.argmax(x >= col(start_x), axis=1),
+            np.abs(x - col(end_x)).argmin(axis=1))
+
+
+def window_lengths(dt, prm):
+    """(w, hop, nsamp) for a sample interval dt (XCORR_* bookkeeping, modules/utils.py:255-257), with the
+    reference's ValueError when int(wlen // dt) != int(wlen / dt) (SURVEY §3-D, dt == 0.004)."""
+    w = int(prm.wlen / dt)
+    w_alloc = int(prm.wlen // dt)
+    if w != w_alloc:
+        raise ValueError(f"could not broadcast input array from shape (1,{w}) into shape ({w_alloc},): "
+                         f"int(wlen // dt) != int(wlen / dt) for dt = {dt!r}")
+    if w < 2:
+        raise ValueError(f"correlation window too short: w={w}")
+    return w, int(w * (1 - 0.5)), int(prm.time_window_to_xcorr // dt)
+
+
 @dataclasses.dataclass(frozen=True)
 class VsgParams:
     """Keyword surface of construct_shot_gather (apis/virtual_shot_gather.py:165-166) + VirtualShotGather."""
@@ -177,33 +227,13 @@ class VsgPlan:
         return cls(geoms, prm, n_ch, n_t)
 
     def nwin(self):
-        L = self.seg_tab[..., 1].astype(np.int64)
-        return np.where(L >= self.w, (L - self.w) // self.hop + 1, 0)
+        return seg_nwin(self.seg_tab, self.w, self.hop)
 
     def algorithmic_bytes(self, out_rows=0):
         """Bytes a launch must move: every receiver sample under a sub-window, each distinct pivot
         sample of a pass once, and out_rows gather rows of w fp32 written."""
-        nw = self.nwin()
-        sides = 2 if self.prm.include_other_side else 1
-        cov = np.where(nw > 0, (nw - 1) * self.hop + self.w, 0)[:, :, :sides]
-        rcv = 4 * int(cov.sum())
-        piv = 0
-        for p in range(self.n_pass):
-            a = self.seg_tab[p, :, :sides, 0].ravel()
-            c = cov[p].ravel()
-            iv = sorted((int(x), int(x + y)) for x, y in zip(a, c) if y > 0)
-            tot, cur_s, cur_e = 0, None, None
-            for s, e in iv:
-                if cur_e is None or s > cur_e:
-                    if cur_e is not None:
-                        tot += cur_e - cur_s
-                    cur_s, cur_e = s, e
-                else:
-                    cur_e = max(cur_e, e)
-            if cur_e is not None:
-                tot += cur_e - cur_s
-            piv += 4 * tot
-        return rcv + piv + 4 * out_rows * self.w
+        return seg_algorithmic_bytes(self.seg_tab, self.w, self.hop, 2 if self.prm.include_other_side else 1,
+                                     out_rows)
 
     def device_tables(self, device):
         key = str(device)
@@ -212,6 +242,122 @@ class VsgPlan:
             self._dev[key] = (torch.from_numpy(np.ascontiguousarray(self.pass_tab)).to(device),
                               torch.from_numpy(np.ascontiguousarray(self.seg_tab)).to(device))
         return self._dev[key]
+
+
+class DevicePlan:
+    """The index tables of one launch derived ON THE DEVICE from the passes' trajectories
+    (dvh_pass_geometry, bit-identical to pass_geometry): the per-pass, per-row float64 work of
+    preprocessing_window / xcorr_two_traces_based_on_traj (apis/virtual_shot_gather.py:111-126, 24-35)
+    runs as a kernel on the launch's stream, so a pipeline forms each batch's tables where it images it.
+
+    The host keeps only what is per channel axis, not per pass: the spatial searches (pivot / start /
+    end index) and (w, hop, nsamp) from dt, with the reference's errors.  Trajectories are device
+    float64 tensors [n, L] (padded; ``trk_len`` [n] int32 valid points, strictly ascending x).
+    ``x_axis`` / ``t_axis`` are shared 1-D arrays or per-pass [n, C] / [n, T] arrays.  Same interface
+    as VsgPlan for the vsg_* entry points (``device_tables``); ``derive()`` (re)launches the kernel,
+    e.g. after the trajectory tensors were refilled for a new batch."""
+
+    def __init__(self, x_axis, t_axis, trk_x, trk_t, trk_len, prm: VsgParams, n_ch: int, pivot_x=None,
+                 start_x=None, end_x=None, derive=True, seg_out=None):
+        import torch
+        self.prm, self.flags = prm, prm.flags
+        x = np.asarray(x_axis, dtype=np.float64)
+        t = np.asarray(t_axis, dtype=np.float64)
+        n = int(trk_x.shape[0])
+        if n == 0:
+            raise ValueError("empty batch")
+        if trk_x.dtype != torch.float64 or trk_t.dtype != torch.float64 or not trk_x.is_cuda:
+            raise ValueError("trajectories must be float64 device tensors [n, L]")
+        if trk_t.shape != trk_x.shape or trk_x.stride(1) != 1 or trk_t.stride() != trk_x.stride():
+            raise ValueError("trk_x / trk_t must share a row-contiguous [n, L] layout")
+        dts = t[..., 1] - t[..., 0]
+        lens = {window_lengths(float(d), prm) for d in np.atleast_1d(dts)}
+        if len(lens) != 1:
+            raise ValueError("passes of one batch must share (w, hop, nsamp); group them first")
+        self.w, self.hop, self.nsamp = lens.pop()
+        piv = np.full(n, float(prm.pivot)) if pivot_x is None else np.asarray(pivot_x, dtype=np.float64)
+        if x.shape[-1] != n_ch or (x.ndim == 2 and x.shape[0] != n) or (t.ndim == 2 and t.shape[0] != n):
+            raise ValueError("x_axis / t_axis must be shared 1-D axes or one row per pass")
+        sx = prm.start_x if start_x is None else np.asarray(start_x, dtype=np.float64)
+        ex = prm.end_x if end_x is None else np.asarray(end_x, dtype=np.float64)
+        if x.ndim == 1 and pivot_x is None and start_x is None and end_x is None:
+            pv, st, en = spatial_indices(x, prm.pivot, sx, ex)
+        else:
+            pv, st, en = spatial_indices(np.broadcast_to(x, (n, x.shape[-1])), piv, sx, ex)
+        pv, st, en = (np.broadcast_to(np.asarray(v), (n,)) for v in (pv, st, en))
+        if not np.all((st <= pv) & (pv < en)):
+            raise ValueError("unsupported gather geometry (need start <= pivot < end)")
+        R = en - st
+        if np.any(R != R[0]):
+            raise ValueError("passes of one batch must share (rows, w, hop); group them first")
+        self.R = int(R[0])
+        self.n_pass, self.n_ch, self.n_t = n, int(n_ch), int(t.shape[-1])
+        if int(en.max()) > self.n_ch:
+            raise ValueError("gather rows beyond the window")
+        dev = trk_x.device
+        self.pass_tab = torch.from_numpy(np.stack([st, pv], 1).astype(np.int32)).to(dev)
+        self.pivot_x = torch.from_numpy(np.ascontiguousarray(piv)).to(dev)
+        self._x = torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+        self._t = torch.from_numpy(np.ascontiguousarray(t)).to(dev)
+        self.trk_x, self.trk_t = trk_x, trk_t
+        self.trk_len = trk_len.to(device=dev, dtype=torch.int32)
+        if seg_out is not None:  # caller-owned table buffer (e.g. shared by a pipeline's batches)
+            if seg_out.dtype != torch.int32 or seg_out.numel() < n * self.R * 4 or not seg_out.is_contiguous():
+                raise ValueError("seg_out must be a contiguous int32 buffer of >= n * R * 4 elements")
+            self.seg_tab = seg_out.view(-1)[:n * self.R * 4].view(n, self.R, 2, 2)
+        else:
+            self.seg_tab = torch.empty((n, self.R, 2, 2), dtype=torch.int32, device=dev)
+        self.status = torch.empty(n, dtype=torch.int32, device=dev)
+        self.geoms = None
+        if derive:
+            self.derive()
+
+    def derive(self):
+        """Launch dvh_pass_geometry on the current stream (asynchronous)."""
+        from . import _lib
+        x_stride = self.n_ch if self._x.dim() == 2 else 0
+        t_stride = self.n_t if self._t.dim() == 2 else 0
+        _lib.call("dvh_pass_geometry", _lib.ptr(self._x), x_stride, _lib.ptr(self._t), t_stride, self.n_t,
+                  _lib.ptr(self.trk_x), _lib.ptr(self.trk_t), self.trk_x.stride(0), _lib.ptr(self.trk_len),
+                  _lib.ptr(self.pivot_x), _lib.ptr(self.pass_tab), self.n_pass, self.R, float(self.prm.delta_t),
+                  self.nsamp, 1 if self.prm.include_other_side else 0, _lib.ptr(self.seg_tab), _lib.ptr(self.status),
+                  _lib.stream_of(self.trk_x.device))
+        return self
+
+    def device_tables(self, device=None):
+        return self.pass_tab, self.seg_tab
+
+    def check(self):
+        """Raise like interp1d would for passes whose trajectory could not be evaluated (synchronises)."""
+        bad = np.nonzero(self.status.cpu().numpy())[0]
+        if bad.size:
+            raise ValueError(f"passes {bad.tolist()[:8]}: trajectory needs >= 2 strictly ascending tracked points")
+        return self
+
+    def host_seg_tab(self):
+        return self.seg_tab.cpu().numpy()
+
+    def nwin(self):
+        return seg_nwin(self.host_seg_tab(), self.w, self.hop)
+
+    def algorithmic_bytes(self, out_rows=0):
+        return seg_algorithmic_bytes(self.host_seg_tab(), self.w, self.hop,
+                                     2 if self.prm.include_other_side else 1, out_rows)
+
+
+def pack_trajectories(trajectories, device):
+    """[(veh_state_x, veh_state_t), ...] -> padded float64 device tensors (trk_x, trk_t [n, L]) and
+    trk_len [n] int32, the layout dvh_pass_geometry reads."""
+    import torch
+    n = len(trajectories)
+    L = max(1, max(len(vx) for vx, _ in trajectories))
+    tx = np.zeros((n, L))
+    tt = np.zeros((n, L))
+    ln = np.zeros(n, dtype=np.int32)
+    for i, (vx, vt) in enumerate(trajectories):
+        k = len(vx)
+        tx[i, :k], tt[i, :k], ln[i] = vx, vt, k
+    return (torch.from_numpy(tx).to(device), torch.from_numpy(tt).to(device), torch.from_numpy(ln).to(device))
 
 
 # ------------------------------------------------------------------------------------------------

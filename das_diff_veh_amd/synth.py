@@ -76,11 +76,12 @@ def linear_trajectory(x_axis_track, speed, tc, pivot):
 
 
 def synth_batch_device(n_pass, n_ch=60, n_t=5500, dx=8.16, x_first=None, t0=DT_W500, dt=0.004, pivot=700.0,
-                       seed=0, device="cuda", n_tones=8, noise=0.05, chunk=64, track_half=350):
+                       seed=0, device="cuda", n_tones=8, noise=0.05, chunk=64, track_half=350, out=None):
     """A batch of synthetic passes generated on the device (same wavefield model as synth_pass,
     fewer tones), for throughput runs.  Returns (windows [n, C, T] float32, x_axis, t_axis,
     per-pass tracked trajectories (veh_state_x, veh_state_t) on the 1 m / 50 Hz tracking grid,
-    speeds)."""
+    speeds).  ``out`` (optional) is a caller-owned [n, C, T] float32 buffer (e.g. a slice of one
+    resident buffer holding several window sets) written in place."""
     import torch
     rng = np.random.default_rng(seed)
     if x_first is None:
@@ -91,7 +92,10 @@ def synth_batch_device(n_pass, n_ch=60, n_t=5500, dx=8.16, x_first=None, t0=DT_W
     tcs = t_axis[n_t // 2] + rng.uniform(-1.0, 1.0, n_pass)
     freqs = rng.uniform(2.0, 25.0, n_tones)
     phases = rng.uniform(0.0, 2.0 * np.pi, (n_pass, n_tones))
-    out = torch.empty((n_pass, n_ch, n_t), dtype=torch.float32, device=device)
+    if out is None:
+        out = torch.empty((n_pass, n_ch, n_t), dtype=torch.float32, device=device)
+    elif tuple(out.shape) != (n_pass, n_ch, n_t) or out.dtype != torch.float32:
+        raise ValueError("out must be a float32 [n_pass, n_ch, n_t] tensor")
     gen = torch.Generator(device=device)
     gen.manual_seed(int(seed) + 12345)
     xs = torch.as_tensor(x_axis, dtype=torch.float32, device=device)[None, :, None]

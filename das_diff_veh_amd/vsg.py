@@ -28,8 +28,11 @@ def _check_windows(windows: torch.Tensor, plan: VsgPlan):
         raise ValueError("windows smaller than the plan or time axis not contiguous")
 
 
-def window_sumsq(windows: torch.Tensor) -> torch.Tensor:
-    out = torch.empty(windows.shape[0], dtype=torch.float64, device=windows.device)
+def window_sumsq(windows: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """||window||_F^2 per pass (float64): the validity of the reference's data / ||data||_F
+    (apis/virtual_shot_gather.py:125) -- NaN / inf anywhere or an all-zero window make the gather NaN."""
+    if out is None:
+        out = torch.empty(windows.shape[0], dtype=torch.float64, device=windows.device)
     _lib.call("dvh_window_sumsq", _lib.ptr(windows), windows.stride(0), windows.stride(1), windows.shape[0],
               windows.shape[1], windows.shape[2], _lib.ptr(out), _lib.stream_of(windows.device))
     return out

@@ -39,6 +39,22 @@ const char* dvh_last_error(void);
 /* FFT length used for correlation windows of w samples (0 if unsupported). */
 int dvh_vsg_fft_length(int32_t w);
 
+/* Per-pass time slices seg_tab[n_pass][R][2][2] derived on the device, float64, with the reference's
+ * expressions (preprocessing_window apis/virtual_shot_gather.py:111-126: interp1d extrapolation of
+ * the trajectory, pt = argmax(t >= f(pivot) +- delta_t); xcorr_two_traces_based_on_traj :24-35: the
+ * per-row t_idx and Python-slice clamping) -- what das_diff_veh_amd.plan.pass_geometry computes on the
+ * host, bit for bit.  Inputs per pass p (strides in elements, 0 = shared by every pass):
+ *   x_axis[p * x_stride + c] channel positions, t_axis[p * t_stride + t] ascending sample times (n_t),
+ *   trajectory trk_x / trk_t[p * trk_stride + k], k < trk_len[p], trk_x strictly ascending,
+ *   pivot_x[p] the `pivot` argument, pass_tab[p] = {row0 = start_idx, pivot_idx} (from the spatial
+ *   searches, which the host does once per channel axis).
+ * flags bit 0: include_other_side.  status[p] = 1 when the trajectory has < 2 points or is not strictly
+ * ascending (interp1d would raise / sort); that pass's rows get empty slices. */
+int dvh_pass_geometry(const double* x_axis, int64_t x_stride, const double* t_axis, int64_t t_stride, int32_t n_t,
+                      const double* trk_x, const double* trk_t, int64_t trk_stride, const int32_t* trk_len,
+                      const double* pivot_x, const int32_t* pass_tab, int32_t n_pass, int32_t R, double delta_t,
+                      int32_t nsamp, int32_t flags, int32_t* seg_tab, int32_t* status, void* stream);
+
 /* ||window||_F^2 per pass (np.linalg.norm(window.data)**2, apis/virtual_shot_gather.py:125). */
 int dvh_window_sumsq(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, int32_t n_ch,
                      int32_t n_t, double* out, void* stream);

@@ -1,0 +1,86 @@
+"""bench.py's own step, at reduced pass counts, against the oracle (not only against itself).
+
+The bench builds its jobs with device-derived tables (dvh_pass_geometry), per-batch validity, one
+resident buffer for several pivots with per-pass channel axes (weights), and batches over a window
+pool with their own trajectories (synth10k, BASELINE configs[2] geometry, R = 1023).  Here the same
+build / step functions run on a few passes and the class stacks and f-v images are compared with
+the float64 oracle (sum(images) / len(images), compute_disp_image).
+"""
+import numpy as np
+import pytest
+
+from tests import golden_io as gio
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def _oracle_classes(job, n_slot):
+    from oracle import vsg as ovsg
+    per_slot = [[] for _ in range(n_slot)]
+    for cs_i, cs in enumerate(job.cpu_sets):
+        host = cs["win"].double().cpu().numpy()
+        for i, (vx, vt) in enumerate(cs["trk"][:host.shape[0]]):
+            o = dict(data=host[i], x_axis=cs["x_axis"], t_axis=cs["t_axis"], veh_state_x=vx, veh_state_t=vt)
+            p = cs["prm"]
+            with np.errstate(all="ignore"):
+                g = ovsg.virtual_shot_gather(o, include_other_side=True, norm=False, pivot=p.pivot, start_x=p.start_x,
+                                             end_x=p.end_x, wlen=p.wlen)[0]
+            per_slot[cs["slots"][i]].append(g)
+    return [ovsg.stack(g) if g else None for g in per_slot]
+
+
+def _check(job, refs, gx, gt):
+    from oracle import disp as odisp
+    got = job.stack.double().cpu().numpy()
+    fv = job.fv.cpu().numpy()
+    for s, ref in enumerate(refs):
+        if ref is None:
+            continue
+        assert gio.gather_rel_err(got[s], ref) < TOL, s
+        fref = odisp.compute_disp_image(ref, gx, gt, start_x=-200, end_x=0)
+        assert np.abs(fv[s] - fref).max() / np.abs(fref).max() < TOL, s
+
+
+def test_weights_job(device):
+    import bench
+    wl = dict(bench.WORKLOADS["weights"], pivots=[(700.0, 500.0, 900.0, (3, 4, 2)), (680.0, 480.0, 880.0, (2, 3, 2))])
+    job = bench.build_resident(wl, device, 1, 0, "weak", chunk=2)
+    bench.step(job, 1)
+    bench.step(job, 1)  # a second step recomputes (tables, validity, stacks) from scratch
+    sl = job.batches[0].slots
+    o = 0
+    for cs in job.cpu_sets:
+        k = cs["win"].shape[0]
+        cs["slots"] = sl[o:o + k]
+        o += k
+    refs = _oracle_classes(job, 6)
+    cs = job.cpu_sets[0]
+    p = cs["prm"]
+    st, pv = int(np.argmax(cs["x_axis"] >= p.start_x)), int(np.argmax(cs["x_axis"] >= p.pivot))
+    R = job.stack.shape[1]
+    dt = cs["t_axis"][1] - cs["t_axis"][0]
+    _check(job, refs, cs["x_axis"][st:st + R] - cs["x_axis"][pv], (np.arange(500) - 250) * dt)
+
+
+def test_synth10k_job(device):
+    import bench
+    wl = dict(bench.WORKLOADS["synth10k"], n_total=6, pool=4, gen_chunk=2)
+    job = bench.build_pool(wl, device, 1, 0, "weak", chunk=2)
+    assert len(job.batches) == 2 and job.batches[0].plan.R == 1023
+    bench.step(job, 1)
+    # pass i of the job lives in pool slot i % 4 during its batch
+    cs = job.cpu_sets[0]
+    slots = np.concatenate([b.slots for b in job.batches])
+    wins = job.windows.double().cpu().numpy()
+    from oracle import vsg as ovsg
+    per_slot = [[] for _ in range(3)]
+    p = cs["prm"]
+    for i, (vx, vt) in enumerate(cs["trk"][:6]):
+        o = dict(data=wins[i % 4], x_axis=cs["x_axis"], t_axis=cs["t_axis"], veh_state_x=vx, veh_state_t=vt)
+        per_slot[slots[i]].append(ovsg.virtual_shot_gather(o, include_other_side=True, norm=False, pivot=p.pivot,
+                                                           start_x=p.start_x, end_x=p.end_x, wlen=p.wlen)[0])
+    refs = [ovsg.stack(g) if g else None for g in per_slot]
+    x = cs["x_axis"]
+    dt = cs["t_axis"][1] - cs["t_axis"][0]
+    _check(job, refs, x[0:1023] - x[512], (np.arange(500) - 250) * dt)

@@ -245,3 +245,23 @@ def test_sliding_geometry_matches_pass_geometry():
     # unit u reads window q's channels at q * C + c of the flattened record
     q, j = plan.unit_window[3], plan.unit_pivot[3]
     assert plan.pass_tab[3, 1] == q * 300 + spatial[0][j]
+
+
+def test_algorithmic_bytes_union_matches_loop():
+    """seg_algorithmic_bytes' vectorised pivot-interval union equals a plain interval merge."""
+    from das_diff_veh_amd.plan import seg_algorithmic_bytes, seg_nwin
+    rng = np.random.default_rng(3)
+    seg = np.zeros((7, 13, 2, 2), dtype=np.int64)
+    seg[..., 0] = rng.integers(0, 3000, seg.shape[:3])
+    seg[..., 1] = rng.choice([0, 400, 500, 999, 1000], seg.shape[:3])
+    w, hop = 500, 250
+    for sides in (1, 2):
+        nw = seg_nwin(seg, w, hop)[:, :, :sides]
+        cov = np.where(nw > 0, (nw - 1) * hop + w, 0)
+        piv = 0
+        for p in range(seg.shape[0]):
+            covered = np.zeros(5000, bool)
+            for a, c in zip(seg[p, :, :sides, 0].ravel(), cov[p].ravel()):
+                covered[a:a + c] = True
+            piv += 4 * int(covered.sum())
+        assert seg_algorithmic_bytes(seg, w, hop, sides, 2) == 4 * int(cov.sum()) + piv + 4 * 2 * w

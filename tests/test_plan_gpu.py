@@ -1,0 +1,102 @@
+"""Device-derived index tables (dvh_pass_geometry) equal the host restatement pass_geometry bit for bit.
+
+pass_geometry (das_diff_veh_amd/plan.py) is itself checked against the reference's slices in
+tests/test_host.py; here the kernel must reproduce it exactly over the golden windows, the synth10k
+geometry of BASELINE configs[2] (R = 1023, most rows' trajectory times outside the window ->
+argmax = 0 reads), early / late / slow passes and per-pass axes.
+"""
+import numpy as np
+import pytest
+
+from tests import golden_io as gio
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(x_axis, t_axis, trks, prm, n_ch, device, pivot_x=None):
+    from das_diff_veh_amd.plan import DevicePlan, VsgPlan, pack_trajectories, pass_geometry
+    xs = x_axis if np.ndim(x_axis) == 2 else [x_axis] * len(trks)
+    ts = t_axis if np.ndim(t_axis) == 2 else [t_axis] * len(trks)
+    geoms = [pass_geometry(x, t, vx, vt, prm) for x, t, (vx, vt) in zip(xs, ts, trks)]
+    host = VsgPlan(geoms, prm, n_ch, len(ts[0]))
+    tx, tt, tl = pack_trajectories(trks, device)
+    dev = DevicePlan(x_axis, t_axis, tx, tt, tl, prm, n_ch, pivot_x=pivot_x).check()
+    assert (dev.R, dev.w, dev.hop, dev.nsamp) == (host.R, host.w, host.hop, host.nsamp)
+    assert np.array_equal(dev.pass_tab.cpu().numpy(), host.pass_tab)
+    got = dev.host_seg_tab()
+    if not np.array_equal(got, host.seg_tab):
+        bad = np.argwhere(got != host.seg_tab)[:5]
+        raise AssertionError(f"seg_tab differs at {bad.tolist()}: {got[tuple(bad[0])]} vs {host.seg_tab[tuple(bad[0])]}")
+    assert dev.algorithmic_bytes(3) == host.algorithmic_bytes(3)
+    return host
+
+
+@pytest.mark.parametrize("fixture", ["vsg_w500", "vsg_w499"])
+@pytest.mark.parametrize("other", [True, False])
+def test_golden_windows(device, fixture, other):
+    from das_diff_veh_amd.plan import VsgParams
+    g = gio.load(fixture)
+    ws = [gio.oracle_window(g, i) for i in range(gio.n_pass(g))]
+    prm = VsgParams(pivot=700, start_x=500, end_x=900, wlen=2, include_other_side=other)
+    _compare(np.stack([w["x_axis"] for w in ws]), np.stack([w["t_axis"] for w in ws]),
+             [(w["veh_state_x"], w["veh_state_t"]) for w in ws], prm, ws[0]["data"].shape[0], device)
+
+
+@pytest.mark.parametrize("case", ["early", "late", "slow", "p680", "narrow", "wlen1"])
+def test_edge_windows(device, case):
+    import ast
+
+    from das_diff_veh_amd.plan import VsgParams
+    g = gio.load("vsg_edge")
+    w = gio.oracle_window(g, 0, prefix=case + "_")
+    kw = ast.literal_eval(str(g[case + "_kw"]))
+    prm = VsgParams(include_other_side=True, norm=False, **kw)
+    _compare(w["x_axis"], w["t_axis"], [(w["veh_state_x"], w["veh_state_t"])], prm, w["data"].shape[0], device)
+
+
+def synth10k_trajectories(x_axis, t_axis, seed, n):
+    """n - 2 regular passes: a slow (15 m/s) and a fast (30 m/s) one whose far rows leave the window,
+    then bench-style ones (15-30 m/s, crossing the pivot within +-1 s of mid-window); and 2 edge passes
+    last: crossing 0.5 s after the window start (other-side shared slice empty: pt - nsamp < 0 wraps,
+    so that side's pivot row is 0 and its rows are x / 0 = +-inf in the reference) and 2 s before its
+    end (forward shared slice shorter than one sub-window: the forward side is +-inf / NaN)."""
+    from das_diff_veh_amd.synth import TRACK_DT
+    rng = np.random.default_rng(seed)
+    xs = np.arange(np.floor(4178.0) - 4300, np.floor(4178.0) + 4301, 1.0)
+    T = t_axis.size
+    specs = [(15.0, t_axis[T // 2]), (30.0, t_axis[T // 2] + 0.3)]
+    specs += [(rng.uniform(15, 30), t_axis[T // 2] + rng.uniform(-1, 1)) for _ in range(max(n - 4, 0))]
+    specs = specs[:max(n - 2, 0)] + [(22.0, t_axis[0] + 0.5), (18.0, t_axis[-1] - 2.0)][:n]
+    return [(xs, np.round((tc + (xs - 4178.0) / v) / TRACK_DT) * TRACK_DT) for v, tc in specs[:n]]
+
+
+def test_synth10k_geometry(device):
+    from das_diff_veh_amd.plan import VsgParams
+    from das_diff_veh_amd.synth import DT_W500
+    x_axis = 0.37 + 8.16 * np.arange(1024)
+    t_axis = DT_W500 + np.arange(8192) * 0.004
+    prm = VsgParams(pivot=4178.0, start_x=0.0, end_x=8400.0, wlen=2, norm=False, include_other_side=True)
+    trks = synth10k_trajectories(x_axis, t_axis, 11, 64)
+    host = _compare(x_axis, t_axis, trks, prm, 1024, device)
+    assert host.R == 1023
+    # the reference's "trajectory time beyond the window -> argmax = 0 -> read [0, nsamp)" quirk is
+    # exercised on most rows
+    f_beyond = sum(int(np.sum(np.interp(x_axis, vx, vt) + 1 > t_axis[-1])) for vx, vt in trks)
+    assert f_beyond > 1000
+
+
+def test_bad_trajectory_status(device):
+    import torch
+
+    from das_diff_veh_amd.plan import DevicePlan, VsgParams, pack_trajectories
+    g = gio.load("vsg_w500")
+    w = gio.oracle_window(g, 0)
+    vx, vt = w["veh_state_x"], w["veh_state_t"]
+    trks = [(vx, vt), (vx[::-1], vt[::-1]), (vx[:1], vt[:1])]
+    tx, tt, tl = pack_trajectories(trks, device)
+    dev = DevicePlan(w["x_axis"], w["t_axis"], tx, tt, tl, VsgParams(pivot=700, start_x=500, end_x=900),
+                     w["data"].shape[0])
+    torch.cuda.synchronize()
+    assert dev.status.cpu().numpy().tolist() == [0, 1, 1]
+    with pytest.raises(ValueError):
+        dev.check()

@@ -19,7 +19,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("vsg_stackf_kernel", "vsg_stack_kernel", "vsg_scales_kernel", "tdft_gemm_kernel", "fk_contract_kernel",
+KERNELS = ("vsg_stackf_kernel", "vsg_stack_kernel", "vsg_scales_kernel", "window_sumsq_kernel", "pass_geometry_kernel", "tdft_gemm_kernel", "fk_contract_kernel",
            "fv_kernel", "fv_batch_kernel", "fv_tile_kernel", "read4", "read16", "atomic4")
 CALIB_BYTES = {"read4": ("FETCH_SIZE", 1 << 30), "read16": ("FETCH_SIZE", 1 << 30), "atomic4": ("WRITE_SIZE", 256 << 20)}
 
@@ -63,10 +63,13 @@ def main():
                 continue
             if "fetch_bytes" in d and "write_bytes" in d:
                 d["traffic_bytes"] = d["fetch_bytes"] * f4 + d["write_bytes"] * fa
+    lay = os.path.join(root, "layout.json")
+    if os.path.exists(lay):  # the bench's launch layout these per-launch counters belong to
+        res["layout"] = json.load(open(lay))
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
-    print(json.dumps({k: {c: v for c, v in d.items() if not str(c).endswith("_dispatches")} for k, d in res.items()},
-                     indent=1))
+    print(json.dumps({k: ({c: v for c, v in d.items() if not str(c).endswith("_dispatches")} if k != "layout" else d)
+                      for k, d in res.items()}, indent=1))
 
 
 if __name__ == "__main__":
