@@ -51,7 +51,7 @@ from das_diff_veh_amd.disp import DispPlan, fk_grid, fv_from_fk  # noqa: E402
 from das_diff_veh_amd.distributed import allreduce_stacks, max_over_ranks, shard_passes  # noqa: E402
 from das_diff_veh_amd.plan import DevicePlan, VsgParams  # noqa: E402
 from das_diff_veh_amd.synth import TRACK_DT, synth_batch_device  # noqa: E402
-from das_diff_veh_amd.vsg import StackSchedule, vsg_scales, vsg_stack, window_sumsq  # noqa: E402
+from das_diff_veh_amd.vsg import StackSchedule, vsg_scales, vsg_stack, vsg_stack_validated, window_sumsq  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # VALU issue peak: 256 CUs x 4 SIMD-32s, one wave64 VALU instruction per 2 cycles per SIMD once >= 2
@@ -108,6 +108,7 @@ class Job:
 
     def finish(self, n_slot, R, w, gx, dt, device):
         self.stack = torch.zeros((n_slot, R, w), dtype=torch.float32, device=device)
+        self.work = torch.empty(max(b.plan.n_pass for b in self.batches) + 1, dtype=torch.int32, device=device)
         s = int(np.abs(gx - (-200.0)).argmin())
         e = int(np.abs(gx - 0.0).argmin())
         self.disp_rows = (s, e + 1)
@@ -307,8 +308,10 @@ def build(workload, device, world, rank, scaling="weak", chunk=8):
 PHASES = ("geometry", "validity", "scales", "stack")
 
 
-def step(job, world, ev=None):
-    """One step; ev (optional) = {phase: list of [start, end] events, one pair per batch}."""
+def step(job, world, ev=None, fused=True):
+    """One step; ev (optional) = {phase: list of [start, end] events, one pair per batch}.  fused: the
+    windows' validity inside the stack launch (vsg_stack_validated); else a window_sumsq launch per
+    batch before the scales."""
     def mark(name, j, k):
         if ev is not None:
             ev[name][j][k].record()
@@ -317,15 +320,19 @@ def step(job, world, ev=None):
         if b.derive:
             b.plan.derive()
         mark("geometry", j, 1)
+        fuse = fused and b.validity and (b.plan.flags & 6)
         mark("validity", j, 0)
-        if b.validity:
+        if b.validity and not fuse:
             window_sumsq(b.win, out=b.sumsq)
         mark("validity", j, 1)
         mark("scales", j, 0)
-        vsg_scales(b.win, b.plan, out=b.scales, win_sumsq=b.sumsq)
+        vsg_scales(b.win, b.plan, out=b.scales, win_sumsq=None if fuse else b.sumsq, validity=not fuse)
         mark("scales", j, 1)
         mark("stack", j, 0)
-        vsg_stack(b.win, b.plan, b.sched, scales=b.scales, out=job.stack, accumulate=j > 0)
+        if fuse:
+            vsg_stack_validated(b.win, b.plan, b.sched, scales=b.scales, out=job.stack, accumulate=j > 0, work=job.work)
+        else:
+            vsg_stack(b.win, b.plan, b.sched, scales=b.scales, out=job.stack, accumulate=j > 0)
         mark("stack", j, 1)
     if world > 1:
         allreduce_stacks([job.stack])
@@ -412,6 +419,7 @@ def cpu_baseline(job, budget_s=20.0, workers=None):
 def layout_of(job, args):
     """What one profiled launch of the stack kernel covers (PMC counters are per launch)."""
     return {"workload": args.workload, "chunk": args.chunk, "scaling": args.scaling,
+            "validity": "separate" if args.separate_validity else "fused",
             "passes_per_launch": [int(b.plan.n_pass) for b in job.batches][:1],
             "launches_per_step": len(job.batches)}
 
@@ -443,6 +451,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--chunk", type=int, default=8, help="passes per stack task (one wave, one gather row)")
+    ap.add_argument("--separate-validity", action="store_true",
+                    help="window_sumsq launch per batch instead of the validity scan inside the stack launch")
     ap.add_argument("--layout-out", default=None, help="write the launch layout (JSON) for tools/pmc_summary.py")
     args = ap.parse_args()
 
@@ -465,16 +475,21 @@ def main():
             json.dump(layout_of(job, args), fh)
 
     for _ in range(args.warmup):
-        step(job, world)
+        step(job, world, fused=not args.separate_validity)
     torch.cuda.synchronize()
     # algorithmic bytes of every stack launch (bookkeeping outside the timed region: the tables of
     # the last derived batch are on the device; re-derive each and copy it back once)
-    bytes_stack = []
+    fused = [bool(not args.separate_validity and b.validity and (b.plan.flags & 6)) for b in job.batches]
+    corr_bytes, win_bytes = [], []
+    out_bytes = 4 * job.stack.shape[0] * job.stack.shape[1] * job.stack.shape[2]
     for b in job.batches:
         if b.derive:
             b.plan.derive()
-        bytes_stack.append(b.plan.algorithmic_bytes(out_rows=job.stack.shape[0] * job.stack.shape[1]))
-    win_bytes = [4 * b.win.shape[0] * b.win.shape[1] * b.win.shape[2] if b.validity else 0 for b in job.batches]
+        corr_bytes.append(b.plan.algorithmic_bytes(out_rows=job.stack.shape[0] * job.stack.shape[1]))
+        win_bytes.append(4 * b.win.shape[0] * b.win.shape[1] * b.win.shape[2] if b.validity else 0)
+    # a validated launch must read every window sample once (the correlation slices are subsets of
+    # the window): its algorithmic bytes are the windows plus the stack rows written
+    bytes_stack = [wb + out_bytes if f else cb for f, wb, cb in zip(fused, win_bytes, corr_bytes)]
     torch.cuda.synchronize()
 
     nb = len(job.batches)
@@ -485,7 +500,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(job, world, ev[k])
+        step(job, world, ev[k], fused=not args.separate_validity)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -502,7 +517,8 @@ def main():
     launch_s = float(ms["stack"].mean()) / 1e3
     achieved = bytes_per_launch / launch_s / 1e9
     layout = layout_of(job, args)
-    traffic, traffic_src = pmc_lookup("vsg_stackf_kernel", layout, "traffic_bytes")
+    kname = "vsg_stackv_kernel" if all(fused) else "vsg_stackf_kernel"
+    traffic, traffic_src = pmc_lookup(kname, layout, "traffic_bytes")
     step_ms = elapsed / args.steps * 1e3
     res = {
         "metric": "vehicle-pass windows/sec -> stacked VSG + f-v images/sec; % HBM/MFMA roofline",
@@ -526,18 +542,23 @@ def main():
         "images_per_s": images_per_step * args.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "vsg_stackf_kernel", "bytes_per_launch": bytes_per_launch,
-                     "launch_ms": launch_s * 1e3},
+                     "kernel": "vsg_stackv_kernel" if all(fused) else "vsg_stackf_kernel",
+                     "bytes_per_launch": bytes_per_launch, "launch_ms": launch_s * 1e3,
+                     "bytes_model": "every window sample once + stack rows written (validity read fused into the "
+                                    "launch)" if all(fused) else "receiver samples under sub-windows + distinct pivot "
+                                    "samples + stack rows written",
+                     "correlation_bytes_per_launch": float(np.mean(corr_bytes)),
+                     "correlation_frac": float(np.mean(corr_bytes)) / launch_s / 1e9 / HBM_PEAK_GBS},
         "step_breakdown_ms": {p: float(ms[p].sum(axis=1).mean()) for p in PHASES},
         "host_setup_s": job.t_plan,
     }
     res["step_breakdown_ms"]["fv_allreduce_rest"] = step_ms - sum(res["step_breakdown_ms"].values())
-    if any(win_bytes):
+    if any(win_bytes) and not any(fused):
         vs = float(ms["validity"].mean()) / 1e3
         res["validity_roofline"] = {"kernel": "window_sumsq_kernel", "bytes_per_launch": float(np.mean(win_bytes)),
                                     "launch_ms": vs * 1e3, "achieved": float(np.mean(win_bytes)) / vs / 1e9,
                                     "frac": float(np.mean(win_bytes)) / vs / 1e9 / HBM_PEAK_GBS}
-    valu, valu_src = pmc_lookup("vsg_stackf_kernel", layout, "SQ_INSTS_VALU")
+    valu, valu_src = pmc_lookup(kname, layout, "SQ_INSTS_VALU")
     res["valu_roofline"] = {"achieved": None if valu is None else valu / launch_s, "peak": VALU_PEAK_INSTR_S,
                             "unit": "wave-instr/s", "frac": None if valu is None else valu / launch_s / VALU_PEAK_INSTR_S,
                             "instr_per_launch": valu, "source": valu_src, "clock_assumed_ghz": 2.4,

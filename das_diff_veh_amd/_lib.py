@@ -27,6 +27,8 @@ SIGNATURES = {
     "dvh_vsg_scales": [_p, _i64, _i64, _i32, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p],
     "dvh_vsg_gathers": [_p, _i64, _i64, _i32, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p],
     "dvh_vsg_stack": [_p, _i64, _i64, _i32, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p],
+    "dvh_vsg_stack_validated": [_p, _i64, _i64, _i32, _i32, _i32, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _i32,
+                                _i32, _p, _p, _p, _p],
     "dvh_disp_row_l1": [_p, _i64, _i64, _i32, _i32, _i32, _p, _p],
     "dvh_disp_tdft": [_p, _i64, _i64, _i32, _i32, _i32, _p, _i32, _p, _p, _p],
     "dvh_disp_fk": [_p, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p],

@@ -341,15 +341,13 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stack_kernel(V
 // (alpha, beta) = (1/2, 1/2) when the other side is finite and non-zero, else (1, 0).  One inverse
 // transform per (chunk, row) replaces the per-pass inverse transform and epilogue.  Passes with a
 // non-finite scale or NaN data go through the exact time-domain path (row_epilogue) instead.
+// The row tasks t0, t0 + stride, ... < n_chunk * R of one wave (task = (chunk, row)).
 template <class E>
-__global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
-    VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
-    const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
-    float* __restrict__ stack) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  E eng = make_engine<E>(lds);
+__device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
+                                             const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
+                                             int32_t n_chunk, const float* __restrict__ weight,
+                                             float* __restrict__ stack, int64_t t0, int64_t stride) {
   const int lane_ = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
   constexpr int N = E::NFFT;
@@ -357,8 +355,7 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
   const bool norm = (A.flags & kFlagNorm) != 0;
   const int h = N / 2;
   const int64_t n_task = (int64_t)n_chunk * A.R;
-  const int64_t stride = (int64_t)gridDim.x * E::kWaves;
-  for (int64_t t = (int64_t)xcd_block() * E::kWaves + wave; t < n_task; t += stride) {
+  for (int64_t t = t0; t < n_task; t += stride) {
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = uni(chunk_tab[3 * c]), e = uni(chunk_tab[3 * c + 1]), slot = uni(chunk_tab[3 * c + 2]);
     int np = -1, ni = 0;
@@ -462,6 +459,164 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
     }
     wave_sync();
   }
+}
+
+template <class E>
+__global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
+    VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
+    const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
+    float* __restrict__ stack) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  E eng = make_engine<E>(lds);
+  const int wave = threadIdx.x >> 6;
+  stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave,
+                  (int64_t)gridDim.x * E::kWaves);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Window validity fused into the stack launch.  The reference divides every window by ||data||_F
+// (preprocessing_window, apis/virtual_shot_gather.py:125): a NaN or inf anywhere in the window, or
+// an all-zero window, makes the whole gather NaN (norm / norm_amp divide by a NaN or zero maximum
+// afterwards), and so its class mean.  Deciding that needs every sample of the window, 4x - 30x the
+// bytes the correlations read.  In the validated stack launch, besides the correlation waves, one
+// wave per block streams the windows (16 x 16-byte loads per lane in flight) and keeps the maximum
+// of |x| as a bit pattern, max(bits & 0x7fffffff): >= 0x7f800000 means a NaN / inf, 0 means all
+// zero.  Work is pulled in units of kScanRows channel rows from a global counter, by the scan waves
+// from the start and by the correlation waves once their row tasks are done, so the HBM-bound scan
+// runs under the VALU-bound transforms.  vsg_invalid_fill_kernel then sets the class slots holding an
+// invalid pass to NaN.
+constexpr int kScanRows = 16;
+#ifndef DVH_SCAN_DEPTH
+#define DVH_SCAN_DEPTH 16
+#endif
+constexpr int kScanDepth = DVH_SCAN_DEPTH;
+
+__device__ __forceinline__ uint32_t absbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+
+__device__ __forceinline__ int pull_unit(uint32_t* counter, int lane) {
+  int u = 0;
+  if (lane == 0) u = (int)atomicAdd(counter, 1u);
+  return __builtin_amdgcn_readfirstlane(__shfl(u, 0));
+}
+
+// Buffer descriptor over [p, p + bytes) built from wave-uniform values (no waterfall loops around the
+// loads); out-of-range loads return 0, which leaves a max |x| unchanged.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t scan_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* pu = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pu, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// max |x| bit pattern over nf4 consecutive float4 (16-byte aligned): unconditional 16-byte buffer
+// loads, kScanDepth per lane in flight (the descriptor's range check zeroes the tail)
+__device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int nf4, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = scan_rsrc(q, (uint32_t)nf4 * 16u);
+  const int nsteps = (nf4 + 63) >> 6;
+  uint32_t m = 0;
+  int off = lane * 16;
+  u32x4 r[kScanDepth];
+#pragma unroll
+  for (int d = 0; d < kScanDepth; ++d) {
+    r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    off += 1024;
+  }
+  for (int s0 = 0; s0 < nsteps; s0 += kScanDepth) {
+#pragma unroll
+    for (int d = 0; d < kScanDepth; ++d) {
+      const u32x4 v = r[d] & 0x7fffffffu;
+      m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      off += 1024;
+    }
+  }
+  return m;
+}
+
+// rows [c0, c1) of a window (n_t samples each): max |x| bit pattern over the wave
+__device__ __forceinline__ uint32_t scan_rows(const float* __restrict__ base, int64_t ch_stride, int c0, int c1,
+                                              int n_t, bool vec, int lane) {
+  uint32_t m = 0;
+  if (vec && ch_stride == n_t) {  // the unit's rows are one contiguous span
+    m = scan_span(base + (int64_t)c0 * ch_stride, ((c1 - c0) * n_t) >> 2, lane);
+  } else if (vec) {
+    for (int c = c0; c < c1; ++c) m = max(m, scan_span(base + (int64_t)c * ch_stride, n_t >> 2, lane));
+  } else {
+    for (int c = c0; c < c1; ++c)
+      for (int t = lane; t < n_t; t += 64) m = max(m, absbits(base[(int64_t)c * ch_stride + t]));
+  }
+  return wave_max_u32(m);
+}
+
+// Pull scan units (pass, kScanRows channel rows) until none is left; atomicMax into vflag[pass].
+__device__ __forceinline__ void scan_units(const VsgArgs& A, int n_ch, int n_t, uint32_t* __restrict__ vflag,
+                                           uint32_t* __restrict__ counter, int lane) {
+  const int upp = (n_ch + kScanRows - 1) / kScanRows;  // units per pass
+  const int n_units = A.n_pass * upp;
+  const bool vec = (n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
+                   (reinterpret_cast<uintptr_t>(A.win) % 16 == 0);
+  int u = pull_unit(counter, lane);
+  while (u < n_units) {
+    const int un = pull_unit(counter, lane);  // the next unit's index, fetched under this unit's loads
+    const int p = u / upp, c0 = (u - p * upp) * kScanRows;
+    const int c1 = min(c0 + kScanRows, n_ch);
+    const uint32_t m = scan_rows(A.win + (int64_t)p * A.pass_stride, A.ch_stride, c0, c1, n_t, vec, lane);
+    if (lane == 0) atomicMax(vflag + p, m);
+    u = un;
+  }
+}
+
+// Persistent validated stack launch: blocks of kFft correlation waves + kScan scan waves, two per CU.
+template <class E, int kFft, int kScan>
+__global__ __launch_bounds__(64 * (kFft + kScan), 4) void vsg_stackv_kernel(
+    VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
+    const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
+    float* __restrict__ stack, int32_t n_ch, int32_t n_t, uint32_t* __restrict__ vflag, uint32_t* __restrict__ counter) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  E eng = make_engine<E>(lds);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave < kFft)
+    stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
+                    (int64_t)gridDim.x * kFft);
+  scan_units(A, n_ch, n_t, vflag, counter, lane);
+}
+
+// The validity scan alone (correlation engines without a validated stack kernel).
+__global__ __launch_bounds__(256) void window_scan_kernel(VsgArgs A, int32_t n_ch, int32_t n_t,
+                                                          uint32_t* __restrict__ vflag, uint32_t* __restrict__ counter) {
+  scan_units(A, n_ch, n_t, vflag, counter, threadIdx.x & 63);
+}
+
+// stack[slot] = NaN for every slot holding a pass whose window is invalid (vflag NaN / inf or 0).
+// Block (slot, part): the slot's passes are found through chunk_tab; part j fills elements
+// [j * 4096, (j + 1) * 4096) of the slot.
+constexpr int kFillBlock = 256;
+__global__ __launch_bounds__(kFillBlock) void vsg_invalid_fill_kernel(const int32_t* __restrict__ order,
+                                                                      const int32_t* __restrict__ chunk_tab,
+                                                                      int32_t n_chunk, const uint32_t* __restrict__ vflag,
+                                                                      float* __restrict__ stack, int64_t slot_elems) {
+  const int slot = blockIdx.y;
+  int bad = 0;
+  for (int c = threadIdx.x; c < n_chunk; c += kFillBlock) {
+    if (chunk_tab[3 * c + 2] != slot) continue;
+    for (int q = chunk_tab[3 * c]; q < chunk_tab[3 * c + 1]; ++q) {
+      const uint32_t f = vflag[order[q]];
+      bad |= (f >= 0x7f800000u) || (f == 0u);
+    }
+  }
+  if (!__syncthreads_or(bad)) return;
+  float* o = stack + (int64_t)slot * slot_elems;
+  const int64_t e0 = (int64_t)blockIdx.x * 4096;
+  for (int64_t k = e0 + threadIdx.x; k < min(e0 + 4096, slot_elems); k += kFillBlock) o[k] = NAN;
 }
 
 // Sum of squares of each pass window (np.linalg.norm(window.data) ** 2), for norm=norm_amp=False.
@@ -636,6 +791,67 @@ DVH_API int dvh_vsg_gathers(const float* win, int64_t pass_stride, int64_t ch_st
   const int64_t grid = (tasks + k.waves - 1) / k.waves;
   void* args[] = {&A, &scales, &out};
   return launch(k.gather, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, (hipStream_t)stream);
+}
+
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      n = v;
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+#ifndef DVH_VSTACK_FFT
+#define DVH_VSTACK_FFT 7  // correlation waves per block of the validated stack launch
+#endif
+#ifndef DVH_VSTACK_SCAN
+#define DVH_VSTACK_SCAN 1  // scan waves per block
+#endif
+
+DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass,
+                                    int32_t n_ch, int32_t n_t, const int32_t* pass_tab, const int32_t* seg_tab, int32_t R,
+                                    int32_t w, int32_t hop, int32_t flags, const float* scales, const int32_t* order,
+                                    const int32_t* chunk_tab, int32_t n_chunk, int32_t n_slot, const float* weight,
+                                    float* stack, uint32_t* work, void* stream) {
+  VsgArgs A{win, pass_stride, ch_stride, pass_tab, seg_tab, n_pass, R, w, hop, flags};
+  if (int rc = check_common(A)) return rc;
+  if (!scales || !order || !chunk_tab || !weight || !stack || !work) return set_error(-2, "null pointer argument");
+  if (!(flags & (kFlagNorm | kFlagNormAmp)))
+    return set_error(-2, "validated stacking needs norm or norm_amp (raw scales need ||data||_F: dvh_window_sumsq)");
+  if (n_ch < R || n_t <= 0) return set_error(-2, "window smaller than the gather");
+  VsgKernels k;
+  int n;
+  if (!get_kernels(w, &k, &n)) return set_error(-4, "unsupported correlation window length");
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t* vflag = work;
+  uint32_t* counter = work + n_pass;
+  hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t) * ((size_t)n_pass + 1), s);
+  if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+  const int64_t tasks = (int64_t)n_chunk * R;
+  if (n == 500 && DVH_FREQ_STACK) {
+    constexpr int F = DVH_VSTACK_FFT, S = DVH_VSTACK_SCAN;
+    const void* fn = (const void*)vsg_stackv_kernel<EngF500, F, S>;
+    const size_t lds = EngF500::kBlockBytes + F * EngF500::kWaveBytes;
+    const int64_t need = (tasks + F - 1) / F;
+    const int grid = (int)(need < 2 * cu_count() ? (need > 0 ? need : 1) : 2 * cu_count());
+    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &n_ch, &n_t, &vflag, &counter};
+    if (int rc = launch(fn, grid, F + S, lds, args, s)) return rc;
+  } else {  // other engines: the scan as its own launch, then the plain stack launch
+    void* sargs[] = {&A, &n_ch, &n_t, &vflag, &counter};
+    if (int rc = launch((const void*)window_scan_kernel, 4 * cu_count(), 4, 0, sargs, s)) return rc;
+    const int64_t grid = (tasks + k.waves - 1) / k.waves;
+    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack};
+    if (int rc = launch(k.stack, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, s)) return rc;
+  }
+  if (n_slot <= 0 || n_chunk <= 0) return 0;
+  const int64_t slot_elems = (int64_t)R * w;
+  hipLaunchKernelGGL(vsg_invalid_fill_kernel, dim3((unsigned)((slot_elems + 4095) / 4096), n_slot), dim3(kFillBlock), 0,
+                     s, order, chunk_tab, n_chunk, (const uint32_t*)vflag, stack, slot_elems);
+  e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
 }
 
 DVH_API int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass,

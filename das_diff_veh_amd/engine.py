@@ -1,55 +1,86 @@
 """Batch engine behind the drop-in classes: windows -> device batches -> HIP kernels.
 
 Windows are grouped by (window shape, gather rows, w, hop) so that each group is one launch of
-each kernel; results come back in the caller's order.
+each kernel; results come back in the caller's order.  Per group, the index tables are derived on
+the device from the windows' trajectories (plan.DevicePlan / dvh_pass_geometry); the host computes
+only what is per channel / time axis (the spatial searches and w, hop, nsamp from dt, with the
+reference's errors).  Class stacks decide the windows' validity (data / ||data||_F,
+apis/virtual_shot_gather.py:125) inside the stack launch (vsg_stack_validated) when norm or norm_amp
+is on, and with a ||window||_F^2 launch otherwise.
 """
 from __future__ import annotations
 
+import dataclasses
+
 import numpy as np
-import torch
 
 from .device import default_device, to_device_f32, to_host_f64
-from .plan import VsgParams, VsgPlan, pass_geometry
-from .vsg import StackSchedule, vsg_gathers, vsg_scales, vsg_stack
+from .plan import DevicePlan, VsgParams, pack_trajectories, spatial_indices, window_lengths
+from .vsg import StackSchedule, vsg_gathers, vsg_stack, vsg_stack_validated
 
 
-def _data_shape(win):
-    d = win.data
-    return tuple(d.shape)
+@dataclasses.dataclass
+class GatherAxes:
+    """The axes of one pass's gather (post_processing_XCF, apis/virtual_shot_gather.py:130-132)."""
+    gather_x_axis: np.ndarray
+    gather_t_axis: np.ndarray
 
 
-def group_windows(windows, prm: VsgParams):
-    geoms = [pass_geometry(w.x_axis, w.t_axis, w.veh_state_x, w.veh_state_t, prm) for w in windows]
+def _axes(win, prm: VsgParams):
+    x = np.asarray(win.x_axis, dtype=np.float64)
+    t = np.asarray(win.t_axis, dtype=np.float64)
+    dt = t[1] - t[0]
+    w, hop, _ = window_lengths(dt, prm)
+    pv, st, en = spatial_indices(x, prm.pivot, prm.start_x, prm.end_x)
+    if not (st <= pv < en):
+        raise ValueError(f"unsupported gather geometry: start_idx={st}, pivot_idx={pv}, end_idx={en} "
+                         f"(need start <= pivot < end)")
+    return (en - st, w, hop), GatherAxes(x[st:en] - x[pv], (np.arange(w) - (w // 2)) * dt)
+
+
+def _shared_or_stacked(arrays):
+    """One 1-D axis when every window has the same one, else the [n, L] stack of them."""
+    a0 = np.asarray(arrays[0], dtype=np.float64)
+    if all(np.array_equal(a0, a) for a in arrays[1:]):
+        return a0
+    return np.stack([np.asarray(a, dtype=np.float64) for a in arrays])
+
+
+def group_windows(windows, prm: VsgParams, device):
+    """[(indices, DevicePlan)] per (data shape, R, w, hop) group, and every pass's GatherAxes."""
+    keys, axes = zip(*[_axes(w, prm) for w in windows]) if windows else ((), ())
     groups = {}
-    for i, (w, g) in enumerate(zip(windows, geoms)):
-        key = (_data_shape(w), g.end_idx - g.start_idx, g.w, g.hop)
-        groups.setdefault(key, []).append(i)
+    for i, (w, k) in enumerate(zip(windows, keys)):
+        groups.setdefault((tuple(w.data.shape),) + k, []).append(i)
     out = []
     for key, idx in groups.items():
-        shape = key[0]
-        out.append((idx, VsgPlan([geoms[i] for i in idx], prm, shape[0], shape[1])))
-    return out, geoms
+        ws = [windows[i] for i in idx]
+        trk = pack_trajectories([(w.veh_state_x, w.veh_state_t) for w in ws], device)
+        plan = DevicePlan(_shared_or_stacked([w.x_axis for w in ws]), _shared_or_stacked([w.t_axis for w in ws]),
+                          *trk, prm, key[0][0])
+        out.append((idx, plan.check()))
+    return out, list(axes)
 
 
 def gathers(windows, prm: VsgParams, device=None):
-    """Per-pass gathers as float64 NumPy arrays, plus each pass's (x_axis, t_axis)."""
+    """Per-pass gathers as float64 NumPy arrays, plus each pass's gather axes."""
     device = device or default_device()
-    groups, geoms = group_windows(windows, prm)
+    groups, axes = group_windows(windows, prm, device)
     res = [None] * len(windows)
     for idx, plan in groups:
         data = to_device_f32([windows[i].data for i in idx], device)
         g = to_host_f64(vsg_gathers(data, plan))
         for k, i in enumerate(idx):
             res[i] = g[k]
-    return res, geoms
+    return res, axes
 
 
 def stacked(windows, prm: VsgParams, slots=None, n_slot=1, device=None, chunk=8):
-    """Class-mean gathers [n_slot, R, w] (device tensor) over all windows."""
+    """Class-mean gathers [n_slot, R, w] (device tensor) over all windows, plus the gather axes."""
     device = device or default_device()
     slots = np.zeros(len(windows), dtype=np.int64) if slots is None else np.asarray(slots)
     counts = np.bincount(slots, minlength=n_slot)
-    groups, geoms = group_windows(windows, prm)
+    groups, axes = group_windows(windows, prm, device)
     keys = {(plan.R, plan.w) for _, plan in groups}
     if len(keys) != 1:
         raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
@@ -57,5 +88,6 @@ def stacked(windows, prm: VsgParams, slots=None, n_slot=1, device=None, chunk=8)
     for idx, plan in groups:
         data = to_device_f32([windows[i].data for i in idx], device)
         sched = StackSchedule(slots[idx], n_slot, chunk=chunk, counts=counts)
-        out = vsg_stack(data, plan, sched, out=out, accumulate=out is not None)
-    return out, geoms
+        fn = vsg_stack_validated if plan.flags & 6 else vsg_stack
+        out = fn(data, plan, sched, out=out, accumulate=out is not None)
+    return out, axes

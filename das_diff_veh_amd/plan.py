@@ -347,7 +347,8 @@ class DevicePlan:
 
 def pack_trajectories(trajectories, device):
     """[(veh_state_x, veh_state_t), ...] -> padded float64 device tensors (trk_x, trk_t [n, L]) and
-    trk_len [n] int32, the layout dvh_pass_geometry reads."""
+    trk_len [n] int32, the layout dvh_pass_geometry reads.  Each trajectory is ordered by x with a
+    stable sort first, as interp1d does (its mergesort of the abscissae)."""
     import torch
     n = len(trajectories)
     L = max(1, max(len(vx) for vx, _ in trajectories))
@@ -355,8 +356,10 @@ def pack_trajectories(trajectories, device):
     tt = np.zeros((n, L))
     ln = np.zeros(n, dtype=np.int32)
     for i, (vx, vt) in enumerate(trajectories):
+        vx, vt = np.asarray(vx, dtype=np.float64), np.asarray(vt, dtype=np.float64)
+        o = np.argsort(vx, kind="mergesort")
         k = len(vx)
-        tx[i, :k], tt[i, :k], ln[i] = vx, vt, k
+        tx[i, :k], tt[i, :k], ln[i] = vx[o], vt[o], k
     return (torch.from_numpy(tx).to(device), torch.from_numpy(tt).to(device), torch.from_numpy(ln).to(device))
 
 

@@ -39,13 +39,16 @@ def window_sumsq(windows: torch.Tensor, out: torch.Tensor | None = None) -> torc
 
 
 def vsg_scales(windows: torch.Tensor, plan: VsgPlan, out: torch.Tensor | None = None,
-               win_sumsq: torch.Tensor | None = None) -> torch.Tensor:
+               win_sumsq: torch.Tensor | None = None, validity: bool = True) -> torch.Tensor:
     """Per-pass scales [n, 2].  ``win_sumsq`` (= window_sumsq(windows), a per-window property that
     callers imaging the same windows repeatedly compute once) also marks windows that are not
-    finite or all zero, whose gathers are NaN in the reference (data / ||data||_F)."""
+    finite or all zero, whose gathers are NaN in the reference (data / ||data||_F); it is computed
+    here when not given, unless ``validity=False`` (the caller decides validity elsewhere, e.g.
+    vsg_stack_validated) and norm or norm_amp is set (the raw mode's scale IS 1 / ||data||_F^2)."""
     _check_windows(windows, plan)
     pass_tab, seg_tab = plan.device_tables(windows.device)
-    sumsq = window_sumsq(windows) if win_sumsq is None else win_sumsq
+    need = validity or not (plan.flags & 6)
+    sumsq = window_sumsq(windows) if (win_sumsq is None and need) else win_sumsq
     if out is None:
         out = torch.empty((plan.n_pass, 2), dtype=torch.float32, device=windows.device)
     _lib.call("dvh_vsg_scales", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
@@ -125,6 +128,37 @@ def vsg_stack(windows: torch.Tensor, plan: VsgPlan, schedule: StackSchedule, sca
               _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop, plan.flags, _lib.ptr(scales),
               _lib.ptr(order), _lib.ptr(chunk_tab), int(chunk_tab.shape[0]), _lib.ptr(weights), _lib.ptr(out),
               _lib.stream_of(windows.device))
+    return out
+
+
+def vsg_stack_validated(windows: torch.Tensor, plan: VsgPlan, schedule: StackSchedule, scales: torch.Tensor | None = None,
+                        out: torch.Tensor | None = None, accumulate: bool = False,
+                        work: torch.Tensor | None = None) -> torch.Tensor:
+    """vsg_stack plus the windows' validity in the same launch (dvh_vsg_stack_validated): every sample
+    of every window [n_ch, n_t] is read once beside the correlations, and a class slot holding a
+    pass whose window has a NaN / inf or is all zero becomes NaN -- the reference's data / ||data||_F
+    (apis/virtual_shot_gather.py:125) -- without a separate ||window||_F pass.  Needs norm or norm_amp
+    (the raw mode's scale is ||data||_F itself: use window_sumsq + vsg_stack).  ``work`` (optional):
+    int32 device buffer of >= n_pass + 1 elements, reused across calls."""
+    _check_windows(windows, plan)
+    if not (plan.flags & 6):
+        raise ValueError("validated stacking needs norm or norm_amp; use window_sumsq + vsg_stack")
+    if windows.shape[1] < plan.R:
+        raise ValueError("windows narrower than the gather")
+    pass_tab, seg_tab = plan.device_tables(windows.device)
+    order, chunk_tab, weights = schedule.device_tables(windows.device)
+    if out is None:
+        out = torch.zeros((schedule.n_slot, plan.R, plan.w), dtype=torch.float32, device=windows.device)
+    elif not accumulate:
+        out.zero_()
+    if scales is None:
+        scales = vsg_scales(windows, plan, validity=False)
+    if work is None or work.numel() < plan.n_pass + 1 or work.dtype != torch.int32:
+        work = torch.empty(plan.n_pass + 1, dtype=torch.int32, device=windows.device)
+    _lib.call("dvh_vsg_stack_validated", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
+              windows.shape[1], windows.shape[2], _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop,
+              plan.flags, _lib.ptr(scales), _lib.ptr(order), _lib.ptr(chunk_tab), int(chunk_tab.shape[0]),
+              schedule.n_slot, _lib.ptr(weights), _lib.ptr(out), _lib.ptr(work), _lib.stream_of(windows.device))
     return out
 
 

@@ -85,6 +85,20 @@ int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stride, int3
                   const int32_t* order, const int32_t* chunk_tab, int32_t n_chunk, const float* weight, float* stack,
                   void* stream);
 
+/* dvh_vsg_stack with the windows' validity decided in the same launch.  The reference divides every
+ * window by ||data||_F (preprocessing_window, apis/virtual_shot_gather.py:125), so a NaN / inf
+ * anywhere in a window [n_ch][n_t], or an all-zero window, makes that pass's gather -- and the mean of
+ * its class -- NaN.  This entry reads every sample of every pass's window once, alongside the
+ * correlations, and sets stack[slot] to NaN for each slot (< n_slot) holding such a pass; the
+ * scales must then come from dvh_vsg_scales WITHOUT win_sumsq.  Requires flags & (norm | norm_amp):
+ * with neither, the scale itself is 1 / ||data||_F^2 (use dvh_window_sumsq).  work: device
+ * workspace of n_pass + 1 uint32 (per-pass max |x| bit pattern, a work counter), zeroed inside. */
+int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, int32_t n_ch,
+                            int32_t n_t, const int32_t* pass_tab, const int32_t* seg_tab, int32_t R, int32_t w,
+                            int32_t hop, int32_t flags, const float* scales, const int32_t* order,
+                            const int32_t* chunk_tab, int32_t n_chunk, int32_t n_slot, const float* weight, float* stack,
+                            uint32_t* work, void* stream);
+
 /* ---------------------------------------------------------------- dispersion (map_fv)
  * Gathers data[B][nch][nt] (strides in elements).  Only the FK bins the (f, k = f / v) queries
  * touch are formed: n_fb frequency bins (twiddles wt[nt][2 * n_fb] = cos | -sin) and n_kb

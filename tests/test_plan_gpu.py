@@ -92,11 +92,15 @@ def test_bad_trajectory_status(device):
     g = gio.load("vsg_w500")
     w = gio.oracle_window(g, 0)
     vx, vt = w["veh_state_x"], w["veh_state_t"]
-    trks = [(vx, vt), (vx[::-1], vt[::-1]), (vx[:1], vt[:1])]
+    # reversed: sorted like interp1d's mergesort -> the same tables; a repeated abscissa (interp1d would
+    # divide by zero) and a single point (interp1d raises) are flagged
+    trks = [(vx, vt), (vx[::-1], vt[::-1]), (np.r_[vx[:5], vx[4:]], np.r_[vt[:5], vt[4:]]), (vx[:1], vt[:1])]
     tx, tt, tl = pack_trajectories(trks, device)
     dev = DevicePlan(w["x_axis"], w["t_axis"], tx, tt, tl, VsgParams(pivot=700, start_x=500, end_x=900),
                      w["data"].shape[0])
     torch.cuda.synchronize()
-    assert dev.status.cpu().numpy().tolist() == [0, 1, 1]
+    assert dev.status.cpu().numpy().tolist() == [0, 0, 1, 1]
+    seg = dev.host_seg_tab()
+    assert np.array_equal(seg[0], seg[1])
     with pytest.raises(ValueError):
         dev.check()

@@ -125,3 +125,19 @@ def test_invalid_window_outside_rows(batch, refs):
                     win_sumsq=batch["sumsq_nan"]).double().cpu().numpy()
     assert np.isnan(got[1]).all()
     assert gio.gather_rel_err(got[0], ovsg.stack([refs[0], refs[2]])) < TOL
+
+
+def test_validated_stack(batch, refs):
+    """The stack launch that also decides every window's validity (vsg_stack_validated) equals the
+    oracle, and a NaN in a channel no gather row reads turns exactly its class NaN."""
+    from das_diff_veh_amd.vsg import StackSchedule, vsg_stack_validated
+    from oracle import vsg as ovsg
+    slots = np.array([0, 1, 0, 1, 2, 2])
+    for key, bad in (("win", None), ("win_nan", 1)):
+        got = vsg_stack_validated(batch[key], batch["plan"], StackSchedule(slots, 3, chunk=2)).double().cpu().numpy()
+        for s in range(2):
+            if s == bad:
+                assert np.isnan(got[s]).all()
+            else:
+                ref = ovsg.stack([refs[i] for i in np.where(slots == s)[0]])
+                assert gio.gather_rel_err(got[s], ref) < TOL, (key, s)

@@ -121,3 +121,40 @@ def test_stack_modes(device, fixture, kw, special):
         with np.errstate(all="ignore"):
             ref = ovsg.stack(refs)
         assert gio.gather_rel_err(got[s], ref) < TOL, (s, kw)
+
+
+@pytest.mark.parametrize("kind", ["zero", "nan", "inf", "nan_outside_rows"])
+def test_validated_stack_invalid_windows(device, kind):
+    """vsg_stack_validated: an all-zero window, or a NaN / inf anywhere in it (also in channels no gather
+    row reads), makes its class mean NaN (data / ||data||_F, apis/virtual_shot_gather.py:125); the
+    other class is unaffected and equals the oracle."""
+    import torch
+
+    from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+    from das_diff_veh_amd.engine import group_windows
+    from das_diff_veh_amd.plan import VsgParams
+    from das_diff_veh_amd.vsg import StackSchedule, vsg_stack_validated
+    from oracle import vsg as ovsg
+    g = gio.load("vsg_w500")
+    n = gio.n_pass(g)
+    arrs = [gio.pass_arrays(g, i) for i in range(n)]
+    d = arrs[1]["data"].copy()
+    if kind == "zero":
+        d[:] = 0
+    elif kind == "nan":
+        d[10, 2000] = np.nan
+    elif kind == "inf":
+        d[30, 100] = np.inf
+    else:
+        d[-1, -1] = np.nan  # the last channel is beyond end_x: no gather row reads it
+    arrs[1]["data"] = d
+    wins = [SurfaceWaveWindow(**a) for a in arrs]
+    prm = VsgParams(include_other_side=True, norm=False, **KW)
+    (idx, plan), = group_windows(wins, prm, device)[0]
+    data = torch.as_tensor(np.stack([w.data for w in wins]), dtype=torch.float32, device=device)
+    slots = np.array([i % 2 for i in range(n)])
+    got = vsg_stack_validated(data, plan, StackSchedule(slots[idx], 2, chunk=2)).double().cpu().numpy()
+    assert np.isnan(got[1]).all()
+    refs = [ovsg.virtual_shot_gather(gio.oracle_window(g, i), include_other_side=True, norm=False, **KW)[0]
+            for i in range(n) if slots[i] == 0]
+    assert gio.gather_rel_err(got[0], ovsg.stack(refs)) < TOL
