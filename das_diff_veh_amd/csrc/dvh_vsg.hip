@@ -37,12 +37,10 @@
 namespace dvh {
 
 constexpr int kBlock = 512;  // sumsq kernel
-// waves per SIMD the kernels are compiled for: one 7-wave Eng500 block (145 KB LDS) per CU;
-// the Stockham engines are register-limited to 3
+// waves per SIMD the kernels are compiled for: the Stockham engines are register-limited to 3,
+// EngF500 fits 4
 template <class E> struct Occ { static constexpr int v = 3; };
 template <> struct Occ<EngF500> { static constexpr int v = 4; };
-template <> struct Occ<EngP500> { static constexpr int v = 4; };
-template <> struct Occ<Eng500> { static constexpr int v = 2; };
 #ifndef DVH_STACKF_OCC
 #define DVH_STACKF_OCC 0
 #endif
@@ -55,6 +53,12 @@ template <class E> struct OccF {
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
   return v;
 }
 
@@ -346,7 +350,8 @@ template <class E>
 __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
-                                             float* __restrict__ stack, int64_t t0, int64_t stride) {
+                                             float* __restrict__ stack, int64_t t0, int64_t stride,
+                                             uint32_t* __restrict__ vflag = nullptr) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -370,6 +375,7 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
 #pragma unroll
     for (int m = 0; m < NH; ++m) Gh[m] = make_float2(0.f, 0.f);
     RowTask task = b < e ? make_task(A, uni(order[b]), i) : RowTask{};
+    uint32_t vmine = 0;  // validated launch: lane k holds max |receiver| of the chunk's k-th pass
     for (int q = b; q < e; ++q) {
       const int p = uni(order[q]);
       RowTask tn = task;
@@ -378,6 +384,14 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
       else if (np >= 0) tn = make_task(A, np, ni);
       float2 Cf[NH], Co[NH];
       eng.spectra(task, tn, has_next, A.w, A.hop, Cf, Co);
+      if (vflag) {  // the receiver samples this task loaded are validated here, not re-read by the scan
+        const uint32_t m = uni((int)wave_max_u32(eng.rmax));
+        if (q - b < 64) {
+          if (lane_ == q - b) vmine = m;
+        } else if (lane_ == 0) {
+          atomicMax(vflag + p, m);
+        }
+      }
       const float sf = unif(scales[2 * p]), so = unif(scales[2 * p + 1]), wp = unif(weight[p]);
       // per-pass bin / twiddle-index math recomputed here (hoisted, it only spills)
       const int lane = opaque(lane_);
@@ -447,6 +461,7 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
       }
       task = tn;
     }
+    if (vflag && lane_ < min(e - b, 64)) atomicMax(vflag + order[b + lane_], vmine);
     float2 Z[NH];
 #pragma unroll
     for (int m = 0; m < NH; ++m) Z[m] = make_float2(0.f, 0.f);
@@ -490,14 +505,15 @@ constexpr int kScanRows = 16;
 #define DVH_SCAN_DEPTH 16
 #endif
 constexpr int kScanDepth = DVH_SCAN_DEPTH;
+#ifndef DVH_SCAN_AUX
+#define DVH_SCAN_AUX 2  // cache policy of the scan's buffer loads (2 = nt, 16 = sc1: both bypass L1)
+#endif
+#ifndef DVH_SCAN_COMPLEMENT
+#define DVH_SCAN_COMPLEMENT 0  // skip the blocks the correlation waves validate
+#endif
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
 
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-  return v;
-}
 
 __device__ __forceinline__ int pull_unit(uint32_t* counter, int lane) {
   int u = 0;
@@ -527,7 +543,7 @@ __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int n
   u32x4 r[kScanDepth];
 #pragma unroll
   for (int d = 0; d < kScanDepth; ++d) {
-    r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, DVH_SCAN_AUX);
     off += 1024;
   }
   for (int s0 = 0; s0 < nsteps; s0 += kScanDepth) {
@@ -535,7 +551,7 @@ __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int n
     for (int d = 0; d < kScanDepth; ++d) {
       const u32x4 v = r[d] & 0x7fffffffu;
       m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
-      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, DVH_SCAN_AUX);
       off += 1024;
     }
   }
@@ -557,19 +573,111 @@ __device__ __forceinline__ uint32_t scan_rows(const float* __restrict__ base, in
   return wave_max_u32(m);
 }
 
+// Blocks of kScanBlk samples: the scan reads whole blocks, one wave-wide 16-byte load each.  The rows a
+// correlation wave loads from (its gather row's forward / other-side slices, as far as the sub-windows
+// reach) are validated by that wave (stackf_tasks), so the scan skips the blocks lying entirely inside
+// them and every window byte is fetched from HBM about once.
+constexpr int kScanBlk = 256;
+constexpr int kScanListBytes = kScanRows * 64 * 4;  // per scanning wave: <= 64 blocks per row
+
+__device__ __forceinline__ uint64_t scan_mask(const VsgArgs& A, int p, int c, int n_t) {
+  const int nb = (n_t + kScanBlk - 1) / kScanBlk;
+  const uint64_t all = nb >= 64 ? ~0ull : ((1ull << nb) - 1);
+  const int i = c - A.pass_tab[2 * p];
+  if (i < 0 || i >= A.R) return all;
+  const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
+  int lo[2] = {0, 0}, hi[2] = {0, 0};
+  const int sides = (A.flags & kFlagOtherSide) ? 2 : 1;
+  for (int sd = 0; sd < sides; ++sd) {
+    const int nw = n_subwin(seg[2 * sd + 1], A.w, A.hop);
+    lo[sd] = seg[2 * sd];
+    hi[sd] = nw > 0 ? lo[sd] + (nw - 1) * A.hop + A.w : lo[sd];
+  }
+  if (hi[0] > lo[0] && hi[1] > lo[1] && lo[1] <= hi[0] && lo[0] <= hi[1]) {  // overlapping: one interval
+    lo[0] = min(lo[0], lo[1]);
+    hi[0] = max(hi[0], hi[1]);
+    hi[1] = lo[1];
+  }
+  uint64_t m = all;
+  for (int sd = 0; sd < 2; ++sd) {
+    if (hi[sd] <= lo[sd]) continue;
+    const int b0 = (lo[sd] + kScanBlk - 1) / kScanBlk;                 // first block starting inside
+    const int b1 = hi[sd] >= n_t ? nb : hi[sd] / kScanBlk;             // blocks ending inside
+    for (int b = b0; b < b1; ++b) m &= ~(1ull << b);
+  }
+  return m;
+}
+
+// rows [c0, c1) (<= 64) of window p, rows contiguous (ch_stride == n_t): the rows' block offsets are
+// listed in LDS, then streamed with kScanDepth loads per lane in flight across rows
+__device__ __forceinline__ uint32_t scan_unit_blocks(const VsgArgs& A, int p, int c0, int c1, int n_ch, int n_t,
+                                                     uint32_t* __restrict__ list, int lane) {
+  const int nr = c1 - c0;
+  uint64_t mask = 0;
+  int cnt = 0;
+  if (lane < nr) {
+    mask = scan_mask(A, p, c0 + lane, n_t);
+    cnt = __popcll(mask);
+  }
+  int pre = cnt;  // inclusive prefix over lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(pre, o);
+    if (lane >= o) pre += t;
+  }
+  const int total = __builtin_amdgcn_readfirstlane(__shfl(pre, 63));
+  if (lane < nr) {
+    int k = pre - cnt;
+    const uint32_t row = (uint32_t)(c0 + lane) * (uint32_t)n_t;
+    while (mask) {
+      const int b = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      list[k++] = row + (uint32_t)(b * kScanBlk);
+    }
+  }
+  wave_sync();
+  const uint32_t wbytes = (uint32_t)n_ch * (uint32_t)n_t * 4u;
+  const __amdgpu_buffer_rsrc_t rs = scan_rsrc(A.win + (int64_t)p * A.pass_stride, wbytes);
+  const uint32_t oob = (uint32_t)n_ch * (uint32_t)n_t;  // a block offset past the window: loads return 0
+  uint32_t m = 0;
+  u32x4 r[kScanDepth];
+#pragma unroll
+  for (int d = 0; d < kScanDepth; ++d) {
+    const uint32_t off = d < total ? list[d] : oob;
+    r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((off + 4u * lane) * 4u), 0, DVH_SCAN_AUX);
+  }
+  for (int s0 = 0; s0 < total; s0 += kScanDepth) {
+#pragma unroll
+    for (int d = 0; d < kScanDepth; ++d) {
+      const u32x4 v = r[d] & 0x7fffffffu;
+      m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+      const int sn = s0 + d + kScanDepth;
+      const uint32_t off = sn < total ? list[sn] : oob;
+      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((off + 4u * lane) * 4u), 0, DVH_SCAN_AUX);
+    }
+  }
+  wave_sync();  // the list is rewritten by the next unit
+  return wave_max_u32(m);
+}
+
 // Pull scan units (pass, kScanRows channel rows) until none is left; atomicMax into vflag[pass].
+// list: this wave's LDS scratch of kScanListBytes.
 __device__ __forceinline__ void scan_units(const VsgArgs& A, int n_ch, int n_t, uint32_t* __restrict__ vflag,
-                                           uint32_t* __restrict__ counter, int lane) {
+                                           uint32_t* __restrict__ counter, uint32_t* __restrict__ list, int lane) {
   const int upp = (n_ch + kScanRows - 1) / kScanRows;  // units per pass
   const int n_units = A.n_pass * upp;
   const bool vec = (n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
                    (reinterpret_cast<uintptr_t>(A.win) % 16 == 0);
+  // complement blocks: contiguous rows, <= 64 blocks per row, a window under 4 GiB
+  const bool blocks = DVH_SCAN_COMPLEMENT && vec && A.ch_stride == n_t && n_t >= kScanBlk && n_t <= 64 * kScanBlk &&
+                      (int64_t)n_ch * n_t * 4 < (1ll << 32) && list != nullptr;
   int u = pull_unit(counter, lane);
   while (u < n_units) {
     const int un = pull_unit(counter, lane);  // the next unit's index, fetched under this unit's loads
     const int p = u / upp, c0 = (u - p * upp) * kScanRows;
     const int c1 = min(c0 + kScanRows, n_ch);
-    const uint32_t m = scan_rows(A.win + (int64_t)p * A.pass_stride, A.ch_stride, c0, c1, n_t, vec, lane);
+    const uint32_t m = blocks ? scan_unit_blocks(A, p, c0, c1, n_ch, n_t, list, lane)
+                              : scan_rows(A.win + (int64_t)p * A.pass_stride, A.ch_stride, c0, c1, n_t, vec, lane);
     if (lane == 0) atomicMax(vflag + p, m);
     u = un;
   }
@@ -584,16 +692,22 @@ __global__ __launch_bounds__(64 * (kFft + kScan), 4) void vsg_stackv_kernel(
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (wave < kFft)
+  uint32_t* list;
+  if (wave < kFft) {
     stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
-                    (int64_t)gridDim.x * kFft);
-  scan_units(A, n_ch, n_t, vflag, counter, lane);
+                    (int64_t)gridDim.x * kFft, DVH_SCAN_COMPLEMENT ? vflag : nullptr);
+    list = reinterpret_cast<uint32_t*>(lds + E::kBlockBytes + (size_t)wave * E::kWaveBytes);  // its FFT buffers
+  } else {
+    list = reinterpret_cast<uint32_t*>(lds + E::kBlockBytes + (size_t)kFft * E::kWaveBytes +
+                                       (size_t)(wave - kFft) * kScanListBytes);
+  }
+  scan_units(A, n_ch, n_t, vflag, counter, list, lane);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
 __global__ __launch_bounds__(256) void window_scan_kernel(VsgArgs A, int32_t n_ch, int32_t n_t,
                                                           uint32_t* __restrict__ vflag, uint32_t* __restrict__ counter) {
-  scan_units(A, n_ch, n_t, vflag, counter, threadIdx.x & 63);
+  scan_units(A, n_ch, n_t, vflag, counter, nullptr, threadIdx.x & 63);  // no correlation waves: whole rows
 }
 
 // stack[slot] = NaN for every slot holding a pass whose window is invalid (vflag NaN / inf or 0).
@@ -704,23 +818,13 @@ static int choose_fft(int w, bool* pad) {
   return 0;
 }
 
-#ifndef DVH_VSG500
-#define DVH_VSG500 0
-#endif
-
 static bool get_kernels(int w, VsgKernels* k, int* n_out) {
   bool pad;
   const int n = choose_fft(w, &pad);
   *n_out = n;
   switch (n) {
     case 250: *k = vsg_kernels<EngStockham<250, false>, true>(); return true;
-    case 500:  // 0: fused-stage Stockham (default), 1: 20 x 25 register engine, 2: plain Stockham,
-               // 3: paired 20 x 5 x 5 in-place engine
-      *k = DVH_VSG500 == 1   ? vsg_kernels<Eng500, true>()
-           : DVH_VSG500 == 2 ? vsg_kernels<EngStockham<500, false>, true>()
-           : DVH_VSG500 == 3 ? vsg_kernels<EngP500, true>()
-                             : vsg_kernels<EngF500, true>();
-      return true;
+    case 500: *k = vsg_kernels<EngF500, true>(); return true;  // fused-stage Stockham
     case 1000: *k = vsg_kernels<EngStockham<1000, false>, true>(); return true;
     case 512: *k = vsg_kernels<EngStockham<512, true>, false>(); return true;
     case 1024: *k = vsg_kernels<EngStockham<1024, true>, false>(); return true;
@@ -834,7 +938,8 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   if (n == 500 && DVH_FREQ_STACK) {
     constexpr int F = DVH_VSTACK_FFT, S = DVH_VSTACK_SCAN;
     const void* fn = (const void*)vsg_stackv_kernel<EngF500, F, S>;
-    const size_t lds = EngF500::kBlockBytes + F * EngF500::kWaveBytes;
+    static_assert(EngF500::kWaveBytes >= kScanListBytes, "a correlation wave's buffers hold its scan list");
+    const size_t lds = EngF500::kBlockBytes + F * EngF500::kWaveBytes + S * kScanListBytes;
     const int64_t need = (tasks + F - 1) / F;
     const int grid = (int)(need < 2 * cu_count() ? (need > 0 ? need : 1) : 2 * cu_count());
     void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &n_ch, &n_t, &vflag, &counter};

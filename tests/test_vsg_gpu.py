@@ -123,7 +123,7 @@ def test_stack_modes(device, fixture, kw, special):
         assert gio.gather_rel_err(got[s], ref) < TOL, (s, kw)
 
 
-@pytest.mark.parametrize("kind", ["zero", "nan", "inf", "nan_outside_rows"])
+@pytest.mark.parametrize("kind", ["zero", "nan", "inf", "nan_outside_rows", "inf_in_slice", "nan_in_slice"])
 def test_validated_stack_invalid_windows(device, kind):
     """vsg_stack_validated: an all-zero window, or a NaN / inf anywhere in it (also in channels no gather
     row reads), makes its class mean NaN (data / ||data||_F, apis/virtual_shot_gather.py:125); the
@@ -145,8 +145,18 @@ def test_validated_stack_invalid_windows(device, kind):
         d[10, 2000] = np.nan
     elif kind == "inf":
         d[30, 100] = np.inf
-    else:
+    elif kind == "nan_outside_rows":
         d[-1, -1] = np.nan  # the last channel is beyond end_x: no gather row reads it
+    else:  # inside a forward-side correlation slice of a gather row (checked by the correlation wave)
+        from das_diff_veh_amd.plan import pass_geometry
+        a = arrs[1]
+        w0 = SurfaceWaveWindow(**a)
+        geo = pass_geometry(a["x_axis"], a["t_axis"], w0.veh_state_x, w0.veh_state_t,
+                            VsgParams(include_other_side=True, norm=False, **KW))
+        i = geo.pivot_idx - geo.start_idx + 3
+        t0, L = geo.seg[i, 0]
+        assert L >= 1000
+        d[geo.start_idx + i, t0 + 400] = np.inf if kind == "inf_in_slice" else np.nan
     arrs[1]["data"] = d
     wins = [SurfaceWaveWindow(**a) for a in arrs]
     prm = VsgParams(include_other_side=True, norm=False, **KW)
