@@ -65,24 +65,52 @@ class DispersionImagesFromWindows(ImagesFromWindows):
     def __init__(self, windows, image_cls=SurfaceWaveDispersion):
         super().__init__(windows, image_cls)
 
-    def get_images(self, norm=False, mute_offset=300, mute=True, **imaging_kwargs):
+    def get_images(self, norm=False, mute_offset=300, mute=True, shard_over_ranks=False, group=None,
+                   **imaging_kwargs):
         """Batched flavour-B path: the trajectory mutes of all windows in one launch on a device copy
-        (dvh_mute_traj), then the per-pass f-v maps and their mean on device."""
+        (dvh_mute_traj), then the per-pass f-v maps and their mean on device.
+
+        shard_over_ranks=True (torch.distributed initialised, every rank holding the same window list):
+        each rank images its shard of the passes and one all-reduce of the per-class |FK| sums gives
+        every rank the same ``avg_image`` (dispersion_classes.sharded_dispersion_means).  The per-pass
+        images are not formed on that path: ``images`` is None and ``shard`` lists this rank's passes."""
+        windows = list(self.windows)
+        if shard_over_ranks:
+            from .dispersion_classes import sharded_dispersion_means
+            if imaging_kwargs.get("method", "naive") != "naive":
+                raise ValueError("the sharded flavour-B path images method='naive' windows (the time-lapse default)")
+            kw = {k: v for k, v in imaging_kwargs.items() if k != "method"}
+            fv, self.shard = sharded_dispersion_means(windows, group=group, norm=norm,
+                                                      mute_offset=mute_offset if mute else None, **kw)
+            self.images = None
+            freqs = kw.get("freqs", np.arange(0.8, 25, 0.1))
+            vels = kw.get("vels", np.arange(200, 1200))
+            self.avg_image = SurfaceWaveDispersion._from_fv(windows[0], freqs, vels, "naive", norm,
+                                                            fv[0].to("cpu").numpy())
+            return
         from .dispersion_classes import batched_surface_wave_dispersion
         self.images, self.avg_image = batched_surface_wave_dispersion(
-            list(self.windows), norm=norm, mute_offset=mute_offset if mute else None, **imaging_kwargs)
+            windows, norm=norm, mute_offset=mute_offset if mute else None, **imaging_kwargs)
 
 
 class VirtualShotGathersFromWindows(ImagesFromWindows):
     def __init__(self, windows, image_cls=VirtualShotGather):
         super().__init__(windows, image_cls)
 
-    def get_images(self, norm=False, mute_offset=300, mute=False, **imaging_kwargs):
-        """apis/imaging_classes.py:137-138 forces norm=False, mute=False, then 96-107."""
+    def get_images(self, norm=False, mute_offset=300, mute=False, shard_over_ranks=False, group=None,
+                   **imaging_kwargs):
+        """apis/imaging_classes.py:137-138 forces norm=False, mute=False, then 96-107.
+
+        shard_over_ranks=True (torch.distributed initialised, every rank holding the same window list):
+        each rank stacks its shard of the passes with 1 / (global count) weights and one all-reduce of
+        the partial stack gives every rank the same ``avg_image``; ``shard`` lists this rank's passes."""
         windows = list(self.windows)
         include_other_side = imaging_kwargs.pop("include_other_side", False)
         prm = vsg_params(include_other_side, norm=False, **imaging_kwargs)
-        stack, geoms = engine.stacked(windows, prm)
+        if shard_over_ranks:
+            stack, geoms, self.shard = engine.stacked_sharded(windows, prm, group=group)
+        else:
+            stack, geoms = engine.stacked(windows, prm)
         self.images = _LazyGathers(windows, prm)
         avg = stack[0].detach().to("cpu").numpy().astype(np.float64)
         self.avg_image = VirtualShotGather._from_arrays(windows[0], avg, geoms[0].gather_x_axis,

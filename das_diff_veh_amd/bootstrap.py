@@ -41,11 +41,13 @@ def _sg_ridge():
     return _SG_RIDGE
 
 
-def ridges(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25, vel_max=400, ref_vel=None):
+def ridges(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25, vel_max=400, ref_vel=None,
+           return_picks=False):
     """extract_ridge_ref_idx (modules/utils.py:621-678) for every image of ``fv`` [B, Nvel, Nfreq]
     (device float32, rows in the map's order = ``vels`` reversed) on the band lb <= f < ub.
     ``ref_freq_idx`` indexes the band; ``ref_vel`` is a callable of frequency (or an array over
-    the band).  Returns float64 [B, n_band] on the host."""
+    the band).  Returns float64 [B, n_band] on the host (and the raw picks before the smoothing
+    with return_picks=True)."""
     if not isinstance(fv, torch.Tensor) or not fv.is_cuda or fv.dtype != torch.float32 or fv.dim() != 3:
         raise ValueError("fv must be a float32 device tensor [B, Nvel, Nfreq] (no CPU fallback)")
     freqs = np.asarray(freqs, dtype=np.float64)
@@ -66,20 +68,23 @@ def ridges(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25, vel_m
     if ref_freq_idx is not None and ref_vel is not None:
         vr = ref_vel(freqs[band]) if callable(ref_vel) else np.asarray(ref_vel, dtype=np.float64)
         vref = torch.as_tensor(np.asarray(vr, dtype=np.float64).reshape(nb), device=dev)
-    ref = -1 if ref_freq_idx is None else int(ref_freq_idx)
-    if ref_freq_idx is not None and not 0 <= ref < nb:
+    # ref_freq_idx=None -> vel_max mode (INT32_MIN); a negative index is a Python index into the band,
+    # walked in the reference's loop order (modules/utils.py:662-671)
+    ref = -2 ** 31 if ref_freq_idx is None else int(ref_freq_idx)
+    if ref_freq_idx is not None and not -nb <= ref < nb:
         raise IndexError(f"index {ref} is out of bounds for axis 0 with size {nb}")
     B = fv.shape[0]
     out = torch.empty((B, nb), dtype=torch.float64, device=dev)
     status = torch.zeros(B, dtype=torch.int32, device=dev)
     vel_t = torch.as_tensor(vel_desc, device=dev)
     sg = torch.as_tensor(_sg_ridge(), device=dev)
+    picks = torch.empty((B, nb), dtype=torch.float64, device=dev) if return_picks else None
     _lib.call("dvh_ridge", _lib.ptr(fv), fv.stride(0), B, fv.shape[1], fv.shape[2], c0, nb, _lib.ptr(vel_t), ref,
               float(sigma), float(vel_max), _lib.ptr(vref), _lib.ptr(sg), 25, _lib.ptr(out), _lib.ptr(status),
-              _lib.stream_of(dev))
+              _lib.ptr(picks), _lib.stream_of(dev))
     if int(status.max()) != 0:
         raise ValueError("attempt to get argmax of an empty sequence (no velocity inside a ridge window)")
-    return out.cpu().numpy()
+    return (out.cpu().numpy(), picks.cpu().numpy()) if return_picks else out.cpu().numpy()
 
 
 class GatherCache:

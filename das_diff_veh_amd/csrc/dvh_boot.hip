@@ -110,22 +110,25 @@ constexpr int kMaxBand = 1024;
 
 // One wave per (image b, ridge):  extract_ridge_ref_idx (modules/utils.py:621-678) on the band of
 // columns [c0, c0 + nb) of fv[b] ([nV][nF], rows = velocities in descending order vel[r]).
-//   ref < 0:  vel_max mode, raw picks over rows at/after argmin |vel_max - vel| (no smoothing)
+//   ref == INT32_MIN:  vel_max mode (ref_freq_idx=None), raw picks over rows at/after
+//             argmin |vel_max - vel| (no smoothing)
 //   vref:     per-column reference velocities (ref_vel(freq)), window (vref - sigma, vref + sigma)
 //   else:     pick at column ref over all rows, then walk backward / forward with the window
-//             (v_prev - sigma, v_prev + sigma); savgol(sgl, 2, mode='interp') of the picks.
+//             (v_prev - sigma, v_prev + sigma); -nb <= ref < 0 is a Python index with the reference's
+//             loop order (below); savgol(sgl, 2, mode='interp') of the picks.
 // status[b] = 0, or 1 when a window holds no velocity (np.argmax of an empty slice raises).
 __global__ __launch_bounds__(64) void ridge_kernel(const float* __restrict__ fv, int64_t b_stride, int32_t nV,
                                                    int32_t nF, int32_t c0, int32_t nb, const double* __restrict__ vel,
                                                    int32_t ref, double sigma, double vel_max,
                                                    const double* __restrict__ vref, const double* __restrict__ sg,
-                                                   int32_t sgl, double* __restrict__ out, int32_t* __restrict__ status) {
+                                                   int32_t sgl, double* __restrict__ out, int32_t* __restrict__ status,
+                                                   double* __restrict__ picks) {
   __shared__ double pick[kMaxBand];
   const int b = blockIdx.x, lane = threadIdx.x;
   const float* F = fv + (int64_t)b * b_stride;
   double* o = out + (int64_t)b * nb;
   int err = 0;
-  if (ref < 0) {
+  if (ref == INT32_MIN) {
     // max_idx = argmin |vel_max - vel| (first of equal distances)
     double bd = INFINITY;
     int bi = nV;
@@ -160,6 +163,23 @@ __global__ __launch_bounds__(64) void ridge_kernel(const float* __restrict__ fv,
       err |= r < 0;
       if (lane == 0) pick[i] = r >= 0 ? vel[r] : NAN;
     }
+  } else if (ref < 0) {
+    // a negative reference index is a Python index: out[ref] is column nb + ref, the backward loop
+    // range(ref - 1, -1, -1) is empty, and range(ref + 1, len(freq)) walks columns nb + ref + 1 ..
+    // nb - 1 and then 0 .. nb - 1 again, seeded by out[-1] (modules/utils.py:662-671)
+    const int k0 = nb + ref;
+    const int rr = column_argmax(F, nF, c0 + k0, 0, nV, lane);
+    double v = rr >= 0 ? vel[rr] : NAN;
+    if (lane == 0) pick[k0] = v;
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int i = pass == 0 ? k0 + 1 : 0; i < nb; ++i) {
+        const int r0 = first_below(vel, nV, v + sigma), r1 = first_at_or_below(vel, nV, v - sigma);
+        const int r = column_argmax(F, nF, c0 + i, r0, r1, lane);
+        err |= r < 0;
+        v = r >= 0 ? vel[r] : NAN;
+        if (lane == 0) pick[i] = v;
+      }
+    }
   } else {
     const int rr = column_argmax(F, nF, c0 + ref, 0, nV, lane);
     const double vr = rr >= 0 ? vel[rr] : NAN;  // wave-uniform (every lane holds the reduced row)
@@ -182,6 +202,8 @@ __global__ __launch_bounds__(64) void ridge_kernel(const float* __restrict__ fv,
     }
   }
   __syncthreads();
+  if (picks)  // the raw picks before smoothing (parity checks of each pick)
+    for (int i = lane; i < nb; i += 64) picks[(int64_t)b * nb + i] = pick[i];
   // savgol_filter(picks, sgl, 2) with mode='interp': interior taps h, edge fits el / er
   const int half = sgl / 2;
   const double* h = sg;
@@ -224,16 +246,16 @@ DVH_API int dvh_select_mean(const float* G, int64_t pass_stride, int64_t K, cons
 
 DVH_API int dvh_ridge(const float* fv, int64_t b_stride, int32_t B, int32_t nV, int32_t nF, int32_t c0, int32_t nb,
                       const double* vel, int32_t ref, double sigma, double vel_max, const double* vref,
-                      const double* sg, int32_t sgl, double* out, int32_t* status, void* stream) {
+                      const double* sg, int32_t sgl, double* out, int32_t* status, double* picks, void* stream) {
   if (!fv || !vel || !out || !status) return set_error(-2, "null pointer argument");
   if (nb <= 0 || c0 < 0 || c0 + nb > nF || nV <= 0) return set_error(-2, "invalid band");
   if (nb > kMaxBand) return set_error(-4, "band longer than 1024 frequencies");
-  if (ref >= 0 || vref) {
+  if (ref != INT32_MIN || vref) {
     if (!sg || sgl % 2 == 0 || sgl > nb) return set_error(-4, "savgol window must be odd and <= the band length");
-    if (ref >= nb) return set_error(-2, "reference index outside the band");
+    if (ref >= nb || ref < -nb) return set_error(-2, "reference index outside the band");
   }
   if (B <= 0) return 0;
   hipLaunchKernelGGL(ridge_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, fv, b_stride, nV, nF, c0, nb, vel,
-                     ref, sigma, vel_max, vref, sg, sgl, out, status);
+                     ref, sigma, vel_max, vref, sg, sgl, out, status, picks);
   return last_launch();
 }

@@ -16,4 +16,4 @@ int set_error(int code, const char* msg) {
 
 DVH_API const char* dvh_last_error(void) { return dvh::g_err; }
 
-DVH_API int dvh_abi_version(void) { return 1; }
+DVH_API int dvh_abi_version(void) { return 2; }  // 2: device tables, validated stacking, raw ridge picks

@@ -75,11 +75,13 @@ def gathers(windows, prm: VsgParams, device=None):
     return res, axes
 
 
-def stacked(windows, prm: VsgParams, slots=None, n_slot=1, device=None, chunk=8):
-    """Class-mean gathers [n_slot, R, w] (device tensor) over all windows, plus the gather axes."""
+def stacked(windows, prm: VsgParams, slots=None, n_slot=1, device=None, chunk=8, counts=None):
+    """Class-mean gathers [n_slot, R, w] (device tensor) over all windows, plus the gather axes.
+    ``counts`` [n_slot]: the class sizes the means divide by (default: these windows' own; a rank of a
+    sharded job passes the global ones, distributed.sharded_class_means)."""
     device = device or default_device()
     slots = np.zeros(len(windows), dtype=np.int64) if slots is None else np.asarray(slots)
-    counts = np.bincount(slots, minlength=n_slot)
+    counts = np.bincount(slots, minlength=n_slot) if counts is None else np.asarray(counts)
     groups, axes = group_windows(windows, prm, device)
     keys = {(plan.R, plan.w) for _, plan in groups}
     if len(keys) != 1:
@@ -91,3 +93,28 @@ def stacked(windows, prm: VsgParams, slots=None, n_slot=1, device=None, chunk=8)
         fn = vsg_stack_validated if plan.flags & 6 else vsg_stack
         out = fn(data, plan, sched, out=out, accumulate=out is not None)
     return out, axes
+
+
+def stacked_sharded(windows, prm: VsgParams, slots=None, n_slot=1, group=None, device=None, chunk=8):
+    """stacked() over the ranks of ``group``: every rank holds the same window list; each stacks its
+    shard (distributed.shard_passes) with 1 / global class count weights and one all-reduce of the
+    partial [n_slot, R, w] stacks gives every rank the class means.  Returns (stacks, axes of every
+    window, this rank's pass indices)."""
+    from .distributed import sharded_class_means
+    import torch
+    device = device or default_device()
+    slots = np.zeros(len(windows), dtype=np.int64) if slots is None else np.asarray(slots, dtype=np.int64)
+    keys, axes = zip(*[_axes(w, prm) for w in windows]) if windows else ((), ())
+    if len({k[:2] for k in keys}) != 1:
+        raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
+    R, w = keys[0][:2]
+    counts = np.bincount(slots, minlength=n_slot)
+
+    def partial(mine, _weights):
+        if mine.size == 0:
+            return torch.zeros((n_slot, R, w), dtype=torch.float32, device=device)
+        out, _ = stacked([windows[i] for i in mine], prm, slots[mine], n_slot, device, chunk, counts=counts)
+        return out
+
+    out, mine = sharded_class_means(partial, slots, n_slot, group)
+    return out, list(axes), mine

@@ -137,14 +137,16 @@ int dvh_select_mean(const float* G, int64_t pass_stride, int64_t K, const int32_
                     float* out, int64_t out_stride, void* stream);
 
 /* extract_ridge_ref_idx on the frequency band [c0, c0 + nb) of fv[b] ([nV][nF], b_stride elements
- * apart), rows = velocities vel[nV] strictly descending.  ref < 0: vel_max mode (raw picks below
- * argmin |vel_max - vel|); vref (nullable, [nb]): per-frequency reference velocities; otherwise
- * the walk from column ref with the window (v - sigma, v + sigma).  Picks of the last two modes are
+ * apart), rows = velocities vel[nV] strictly descending.  ref == INT32_MIN: vel_max mode (raw picks
+ * below argmin |vel_max - vel|); vref (nullable, [nb]): per-frequency reference velocities; otherwise
+ * the walk from column ref with the window (v - sigma, v + sigma); -nb <= ref < 0 indexes like Python
+ * (column nb + ref, then the reference's loop order: forward to the end, then 0 .. nb - 1 again).  Picks of the last two modes are
  * smoothed by savgol(sgl, 2) given as sg = {h[sgl], left[sgl/2][sgl], right[sgl/2][sgl]}.
- * out[B][nb] float64; status[b] = 1 when a window held no velocity (the reference raises). */
+ * out[B][nb] float64; status[b] = 1 when a window held no velocity (the reference raises); picks
+ * (nullable, [B][nb] float64) receives the raw picks before the smoothing. */
 int dvh_ridge(const float* fv, int64_t b_stride, int32_t B, int32_t nV, int32_t nF, int32_t c0, int32_t nb,
               const double* vel, int32_t ref, double sigma, double vel_max, const double* vref, const double* sg,
-              int32_t sgl, double* out, int32_t* status, void* stream);
+              int32_t sgl, double* out, int32_t* status, double* picks, void* stream);
 
 /* ---------------------------------------------------------------- preprocessing
  * dtype: 0 float32, 1 float64; data modified in place. */

@@ -17,8 +17,10 @@ from . import disp as odisp
 from . import vsg as ovsg
 
 
-def extract_ridge_ref_idx(freq, vel, fv_map, ref_freq_idx=None, sigma=25, vel_max=400, ref_vel=None):
-    """modules/utils.py:621-678: vel ascending (reversed to the map's row order), fv_map [Nvel, Nfreq]."""
+def extract_ridge_ref_idx(freq, vel, fv_map, ref_freq_idx=None, sigma=25, vel_max=400, ref_vel=None,
+                          return_picks=False):
+    """modules/utils.py:621-678: vel ascending (reversed to the map's row order), fv_map [Nvel, Nfreq].
+    return_picks=True also returns the raw picks before savgol (the walk's per-column argmax)."""
     vel = vel[::-1]
     if ref_freq_idx is None:
         max_idx = np.abs(vel_max - vel).argmin()
@@ -35,7 +37,8 @@ def extract_ridge_ref_idx(freq, vel, fv_map, ref_freq_idx=None, sigma=25, vel_ma
         for i in range(len(freq)):
             mask = (vel > vr[i] - sigma) & (vel < vr[i] + sigma)
             out[i] = vel[mask][np.argmax(fv_map[mask, i])]
-    return scipy.signal.savgol_filter(out, 25, 2)
+    sm = scipy.signal.savgol_filter(out, 25, 2)
+    return (sm, out) if return_picks else sm
 
 
 def bootstrap_disp(wins, bt_size, bt_times, sigma, pivot, start_x, end_x, ref_freq_idx, freq_lb, freq_up, ref_vel,

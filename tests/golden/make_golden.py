@@ -259,6 +259,8 @@ def gen_ridge(ref):
     out["refvel_f"] = np.array([10, 12, 13, 14, 15, 16], float)
     out["refvel_v"] = np.array([530, 470, 450, 430, 410, 391], float)
     out["velmax"] = ref.ut.extract_ridge_ref_idx(freqs[m0], vels, fv[:, m0], sigma=25, vel_max=800)
+    # a negative (Python) reference index: column nb - 7, then the reference's own loop order
+    out["walk_neg7"] = ref.ut.extract_ridge_ref_idx(freqs[m0], vels, fv[:, m0], ref_freq_idx=-7, sigma=25, vel_max=800)
     # bootstrap: two modes (a walk and a reference-curve mode), bt_size 3 of the 4 drawable passes
     random.seed(11)
     rv, fq = ref.ic.bootstrap_disp(wins, 3, 4, [25, 50], 700, 500, 900, [80, 130], [2.5, 10], [14, 15], [None, mode1])
@@ -267,6 +269,39 @@ def gen_ridge(ref):
     out["boot_freqs"] = fq
     random.seed(11)
     out["boot_sel"] = np.array([random.sample(range(1, len(wins)), 3) for _ in range(4)])
+    # the reference's f-v map of every resample (the same draws), for the per-pick parity of bootstrap_disp
+    fvs = []
+    for sel in out["boot_sel"]:
+        imgs = ref.ic.VirtualShotGathersFromWindows([wins[i] for i in sel])
+        imgs.get_images(pivot=700, start_x=500, end_x=900, wlen=2, include_other_side=True)
+        imgs.avg_image.compute_disp_image(end_x=0, start_x=-150)
+        fvs.append(imgs.avg_image.disp.fv_map)
+    out["boot_fv"] = np.stack(fvs).astype(np.float32)
+    return out
+
+
+def gen_fk(ref):
+    """fk (modules/utils.py:236-248): |fftshift(fft2(data, s=[nk, nf]))| and its axes, on the [-200, 0] m
+    rows of the vsg_w500 class stack (the block compute_disp_image images) and on two quantised random
+    blocks with non-power-of-two and power-of-two shapes."""
+    kw = dict(pivot=700, start_x=500, end_x=900, wlen=2)
+    wins = [ref_window(ref, synth_pass(100 + i)) for i in range(5)]
+    images = ref.ic.VirtualShotGathersFromWindows(wins)
+    images.get_images(include_other_side=True, **kw)
+    im = images.avg_image
+    s = np.abs(im.x_axis - (-200)).argmin()
+    e = np.abs(im.x_axis - 0).argmin()
+    out = {}
+    rng = np.random.default_rng(700)
+    cases = {"stack": (im.XCF_out[s:e + 1], 8.16, im.t_axis[1] - im.t_axis[0]),
+             "odd": (np.round(rng.standard_normal((37, 777)) * 2 ** 10) / 2 ** 10, 4.08, 0.002),
+             "pow2": (np.round(rng.standard_normal((32, 512)) * 2 ** 10) / 2 ** 10, 8.16, 0.004)}
+    for name, (data, dx, dt) in cases.items():
+        res, ff, kk = ref.ut.fk(data, dx, dt)
+        out[name + "_data"] = np.asarray(data, dtype=np.float64)
+        out[name + "_dx"], out[name + "_dt"] = np.array(dx), np.array(dt)
+        out[name + "_fk"] = res.astype(np.float32)
+        out[name + "_f"], out[name + "_k"] = ff, kk
     return out
 
 
@@ -349,7 +384,7 @@ def gen_tli(ref):
 
 
 GENERATORS = {"vsg_w500": gen_vsg, "vsg_w499": gen_vsg_w499, "vsg_edge": gen_vsg_edge, "disp": gen_disp,
-              "bandpass": gen_bandpass, "ridge": gen_ridge, "prep": gen_prep, "select": gen_select,
+              "bandpass": gen_bandpass, "ridge": gen_ridge, "fk": gen_fk, "prep": gen_prep, "select": gen_select,
               "tli": gen_tli}
 
 

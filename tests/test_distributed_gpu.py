@@ -82,3 +82,69 @@ def test_two_ranks_one_gpu_stack_reduction(device):
             refs = [ovsg.virtual_shot_gather(gio.oracle_window(g, i), include_other_side=True, norm=False, **KW)[0]
                     for i in np.flatnonzero(slots == c)]
             assert gio.gather_rel_err(stacks[c], ovsg.stack(refs)) < 1e-4
+
+
+def _api_worker(rank, world, port, q):
+    """Both drop-in flavours with shard_over_ranks=True on the ranks of a gloo group (one GPU)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+        from das_diff_veh_amd.apis.imaging_classes import DispersionImagesFromWindows, VirtualShotGathersFromWindows
+        from tests.test_tli_gpu import _tli
+        gd = gio.load("disp")
+        wins = [SurfaceWaveWindow(**gio.pass_arrays(gd, i)) for i in range(gio.n_pass(gd))]
+        imgs = DispersionImagesFromWindows(wins)
+        imgs.get_images(mute_offset=300, freqs=gd["freqs"], vels=gd["vels"], method="naive", start_x=500, end_x=800,
+                        shard_over_ranks=True)
+        assert imgs.images is None and not any(w.muted_along_traj for w in wins)
+        gv = gio.load("vsg_w500")
+        vw = [SurfaceWaveWindow(**gio.pass_arrays(gv, i)) for i in range(gio.n_pass(gv))]
+        vimgs = VirtualShotGathersFromWindows(vw)
+        vimgs.get_images(include_other_side=True, shard_over_ranks=True, **KW)
+        # TimeLapseImaging.get_images forwards the keyword to its DispersionImagesFromWindows
+        import das_diff_veh_amd.apis.timeLapseImaging as tl
+        orig = tl.TimeLapseImaging.get_images
+        tl.TimeLapseImaging.get_images = lambda self, mute_offset=300, **kw: orig(self, mute_offset,
+                                                                                  shard_over_ranks=True, **kw)
+        try:
+            obj, _, _ = _tli()
+        finally:
+            tl.TimeLapseImaging.get_images = orig
+        q.put((rank, imgs.avg_image.disp.fv_map, imgs.shard.tolist(), vimgs.avg_image.XCF_out, vimgs.shard.tolist(),
+               obj.images.avg_image.disp.fv_map))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_one_gpu_sharded_flavours(device):
+    """Flavour B (DispersionImagesFromWindows, TimeLapseImaging 'surface_wave') and flavour A
+    (VirtualShotGathersFromWindows) sharded over 2 ranks: every rank's avg_image equals the reference's
+    single-process result (disp.npz:muted_stack, tli.npz:fv_avg, vsg_w500.npz:stack)."""
+    import socket
+
+    from tests.test_disp_gpu import _check
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_api_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=180) for _ in range(2)), key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(out[0][2] + out[1][2]) == [0, 1, 2]
+    assert sorted(out[0][4] + out[1][4]) == [0, 1, 2, 3, 4]
+    gd, gv, gt = gio.load("disp"), gio.load("vsg_w500"), gio.load("tli")
+    for _, fv, _, xcf, _, tfv in out:
+        _check(fv, gd["muted_stack"])
+        assert gio.gather_rel_err(xcf, gv["stack"]) < 1e-4
+        _check(tfv, gt["fv_avg"])

@@ -152,7 +152,7 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
-    assert _lib.load().dvh_abi_version() == 1
+    assert _lib.load().dvh_abi_version() == 2
     assert _lib.load().dvh_vsg_fft_length(500) == 500
     assert _lib.load().dvh_vsg_fft_length(499) == 1024
     assert _lib.load().dvh_vsg_fft_length(5000) == 0

@@ -131,12 +131,34 @@ def test_oracle_ridge_and_bootstrap_match_reference():
     assert np.array_equal(orid.extract_ridge_ref_idx(fq[m1], vels, fv[:, m1], ref_freq_idx=130 - int(np.sum(fq < 10)),
                                                      sigma=50, vel_max=800, ref_vel=mode1), g["refvel"])
     assert np.array_equal(orid.extract_ridge_ref_idx(fq[m0], vels, fv[:, m0], sigma=25, vel_max=800), g["velmax"])
+    assert np.array_equal(orid.extract_ridge_ref_idx(fq[m0], vels, fv[:, m0], ref_freq_idx=-7, sigma=25, vel_max=800),
+                          g["walk_neg7"])
     v5 = gio.load("vsg_w500")
     wins = [gio.oracle_window(v5, i) for i in range(5)]
     random.seed(11)
     rv, f = orid.bootstrap_disp(wins, 3, 4, [25, 50], 700, 500, 900, [80, 130], [2.5, 10], [14, 15], [None, mode1])
     assert np.abs(np.stack(rv[0]) - g["boot_mode0"]).max() < 1e-9
     assert np.abs(np.stack(rv[1]) - g["boot_mode1"]).max() < 1e-9
+    # the reference's per-resample f-v maps (boot_fv) give its bootstrap ridges through the oracle walk
+    for b in range(4):
+        for m, (lb, ub, ri, sg, vr, key) in enumerate(((2.5, 14, 80, 25, None, "boot_mode0"),
+                                                       (10, 15, 130, 50, mode1, "boot_mode1"))):
+            band = (f >= lb) & (f < ub)
+            r = orid.extract_ridge_ref_idx(f[band], vels, g["boot_fv"][b][:, band], ref_freq_idx=ri - int(np.sum(f < lb)),
+                                           sigma=sg, vel_max=800, ref_vel=vr)
+            assert np.abs(r - g[key][b]).max() < 1e-9, (b, m)
+
+
+@pytest.mark.parametrize("case", ["stack", "odd", "pow2"])
+def test_oracle_fk_matches_reference(case):
+    """oracle/disp.fk against the reference's fk (modules/utils.py:236-248): magnitudes and both axes."""
+    from oracle import disp as odisp
+    g = gio.load("fk")
+    res, ff, kk = odisp.fk(g[case + "_data"], float(g[case + "_dx"]), float(g[case + "_dt"]))
+    ref = g[case + "_fk"].astype(np.float64)
+    assert res.shape == ref.shape
+    assert np.abs(res - ref).max() <= 1e-6 * np.abs(ref).max()
+    assert np.array_equal(ff, g[case + "_f"]) and np.array_equal(kk, g[case + "_k"])
 
 
 @pytest.mark.parametrize("case", ["plain", "dead", "spike", "dead_last", "dead_first_spike"])
