@@ -98,15 +98,29 @@ class VirtualShotGathersFromWindows(ImagesFromWindows):
         super().__init__(windows, image_cls)
 
     def get_images(self, norm=False, mute_offset=300, mute=False, shard_over_ranks=False, group=None,
-                   **imaging_kwargs):
+                   skip_failed=False, **imaging_kwargs):
         """apis/imaging_classes.py:137-138 forces norm=False, mute=False, then 96-107.
 
         shard_over_ranks=True (torch.distributed initialised, every rank holding the same window list):
         each rank stacks its shard of the passes with 1 / (global count) weights and one all-reduce of
-        the partial stack gives every rank the same ``avg_image``; ``shard`` lists this rank's passes."""
+        the partial stack gives every rank the same ``avg_image``; ``shard`` lists this rank's passes.
+        skip_failed=True: a pass whose geometry or trajectory cannot be formed is left out of the mean
+        and reported in ``failed`` {window index: reason} instead of raising for the whole list
+        (engine.stacked_checked); ``images`` then holds the imaged windows' gathers."""
         windows = list(self.windows)
         include_other_side = imaging_kwargs.pop("include_other_side", False)
         prm = vsg_params(include_other_side, norm=False, **imaging_kwargs)
+        self.failed = {}
+        if skip_failed:
+            stack, axes, self.failed = engine.stacked_checked(windows, prm)
+            if stack is None:
+                raise ValueError(f"no pass could be imaged: {self.failed}")
+            good = [i for i in range(len(windows)) if i not in self.failed]
+            self.images = _LazyGathers([windows[i] for i in good], prm)
+            g0 = axes[good[0]]
+            avg = stack[0].detach().to("cpu").numpy().astype(np.float64)
+            self.avg_image = VirtualShotGather._from_arrays(windows[good[0]], avg, g0.gather_x_axis, g0.gather_t_axis)
+            return
         if shard_over_ranks:
             stack, geoms, self.shard = engine.stacked_sharded(windows, prm, group=group)
         else:

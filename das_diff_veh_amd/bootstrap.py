@@ -153,3 +153,37 @@ def bootstrap_ridges(cache: GatherCache, sels, sigma, ref_freq_idx, freq_lb, fre
 def draw(n, bt_size, bt_times, rand=random):
     """The reference's draws: bt_times x random.sample(range(1, n), bt_size)."""
     return np.array([rand.sample(range(1, n), bt_size) for _ in range(bt_times)], dtype=np.int32)
+
+
+def save_ridge_npz(file_name, freqs, freq_lb, freq_ub, reference_layout=False, **ridges):
+    """The ridge-statistics npz of the notebooks (imaging_diff_speed.ipynb#cell27, data/<x0>_speeds.npz:
+    ``freqs, freq_lb, freq_ub, vels_<class>``) for bootstrap_disp results.  ``ridges``: class name ->
+    ridge_vel, bootstrap_disp's list over modes of per-resample ridge arrays (modes have different band
+    lengths).  By default the file is pickle-free: ``vels_<class>`` is omitted and each mode is a dense
+    ``vels_<class>_m<k>`` [n_resample, n_band_k] array (load with allow_pickle=False, load_ridge_npz).
+    reference_layout=True writes ``vels_<class>`` as the notebook's ragged object array instead (np.savez
+    pickles it; only the notebook's own np.load(allow_pickle=True) reads that)."""
+    out = dict(freqs=np.asarray(freqs, dtype=np.float64), freq_lb=np.asarray(freq_lb),
+               freq_ub=np.asarray(freq_ub))
+    for name, per_mode in ridges.items():
+        if reference_layout:
+            arr = np.empty(len(per_mode), dtype=object)
+            for k, rv in enumerate(per_mode):
+                arr[k] = list(rv)
+            out[f"vels_{name}"] = arr
+        else:
+            for k, rv in enumerate(per_mode):
+                out[f"vels_{name}_m{k}"] = np.asarray(rv, dtype=np.float64).reshape(len(rv), -1)
+    np.savez(file_name, **out)
+
+
+def load_ridge_npz(file_name):
+    """(freqs, freq_lb, freq_ub, {class: [per-mode [n_resample, n_band] arrays]}) of a pickle-free
+    save_ridge_npz file (allow_pickle=False)."""
+    with np.load(file_name, allow_pickle=False) as f:
+        ridges = {}
+        for key in sorted(k for k in f.files if k.startswith("vels_")):
+            name, _, m = key[5:].rpartition("_m")
+            ridges.setdefault(name, {})[int(m)] = f[key]
+        return (f["freqs"], f["freq_lb"], f["freq_ub"],
+                {n: [d[k] for k in sorted(d)] for n, d in ridges.items()})

@@ -118,3 +118,47 @@ def stacked_sharded(windows, prm: VsgParams, slots=None, n_slot=1, group=None, d
 
     out, mine = sharded_class_means(partial, slots, n_slot, group)
     return out, list(axes), mine
+
+
+def pass_failures(windows, prm: VsgParams):
+    """Per-pass failure status of a batch, decided on the host before any launch (skip +
+    count): {pass index: reason} for a gather geometry preprocessing_window cannot slice, the
+    dt == 0.004 window-length mismatch, a trajectory interp1d (and dvh_pass_geometry) would reject
+    (< 2 distinct finite tracked points), or a gather shape other than the batch's (that of its first
+    good pass).  Also returns every pass's GatherAxes (None for a failed one)."""
+    failed, keys, axes = {}, {}, [None] * len(windows)
+    for i, w in enumerate(windows):
+        try:
+            keys[i], axes[i] = _axes(w, prm)
+        except ValueError as e:
+            failed[i] = str(e)
+            continue
+        vx, vt = np.asarray(w.veh_state_x, dtype=np.float64), np.asarray(w.veh_state_t, dtype=np.float64)
+        if vx.size < 2 or vx.size != vt.size or not np.all(np.isfinite(vx)) or np.unique(vx).size != vx.size:
+            failed[i] = "trajectory needs >= 2 distinct finite tracked points (interp1d)"
+    ok = [i for i in range(len(windows)) if i not in failed]
+    if ok:
+        rw = keys[ok[0]][:2]
+        for i in ok:
+            if keys[i][:2] != rw:
+                failed[i] = f"gather shape (R, w) = {keys[i][:2]} differs from the batch's {rw}"
+    for i in failed:
+        axes[i] = None
+    return failed, axes
+
+
+def stacked_checked(windows, prm: VsgParams, slots=None, n_slot=1, device=None, chunk=8):
+    """stacked() with a failure status per pass instead of one per batch (skip + count).
+    The reference raises on the first broken window and loses the whole class (a notebook cell dies);
+    here the passes pass_failures() rejects are left out of their classes and reported, and the class
+    means divide by the passes that were imaged.  Returns (stacks [n_slot, R, w] or None when no pass
+    is left, axes per pass (None for a failed one), failed {pass index: reason})."""
+    device = device or default_device()
+    slots = np.zeros(len(windows), dtype=np.int64) if slots is None else np.asarray(slots, dtype=np.int64)
+    failed, axes = pass_failures(windows, prm)
+    ok = np.array([i for i in range(len(windows)) if i not in failed], dtype=np.int64)
+    if ok.size == 0:
+        return None, axes, failed
+    counts = np.bincount(slots[ok], minlength=n_slot)
+    out, _ = stacked([windows[i] for i in ok], prm, slots[ok], n_slot, device, chunk, counts=counts)
+    return out, axes, failed

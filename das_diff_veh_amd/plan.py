@@ -218,7 +218,9 @@ class VsgPlan:
         self.geoms = geoms
         self.pass_tab = np.array([[g.start_idx, g.pivot_idx] for g in geoms], dtype=np.int32)
         self.seg_tab = np.stack([g.seg for g in geoms]).astype(np.int32)  # [n, R, 2, 2]
-        assert self.seg_tab.min() >= 0 and (self.seg_tab[..., 0] + self.seg_tab[..., 1]).max() <= n_t
+        if self.seg_tab.min() < 0 or (self.seg_tab[..., 0] + self.seg_tab[..., 1]).max() > n_t:
+            raise ValueError("time slices outside the window: the passes' t_axis does not match the window's "
+                             f"{n_t} samples")
         self._dev = {}
 
     @classmethod
@@ -486,7 +488,9 @@ class UnitPlan(VsgPlan):
         if self.n_ch >= 2 ** 31:
             raise ValueError("flattened record exceeds int32 channel indices")
         assert self.seg_tab.shape == (self.n_pass, self.R, 2, 2)
-        assert self.seg_tab.min() >= 0 and (self.seg_tab[..., 0] + self.seg_tab[..., 1]).max() <= n_t
+        if self.seg_tab.min() < 0 or (self.seg_tab[..., 0] + self.seg_tab[..., 1]).max() > n_t:
+            raise ValueError("time slices outside the window: the passes' t_axis does not match the window's "
+                             f"{n_t} samples")
         self.geoms = None
         self._dev = {}
 

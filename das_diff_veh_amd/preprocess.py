@@ -125,16 +125,19 @@ def surface_wave_preprocessing(data, dt, method="surface_wave", flo=1.2, fhi=30,
     continuous record [n_ch, n_t] -> ``data_for_imaging`` (a new array; the input is left as is):
     bandpass_data(flo, fhi) (dvh_sosfiltfilt), then find_noise_idx / impute_noisy_trace for an empty
     trace and for a noisy trace, then for method 'surface_wave' the per-trace L2 norm
-    (dvh_trace_cleanup).  Host arrays in -> host arrays out (float64 like the reference); device
-    tensors stay on the device.  With return_indices, also the (empty, noisy) trace indices imputed."""
+    (dvh_trace_cleanup).  Host arrays in -> host arrays out in the record's dtype, like the
+    reference's data.copy(): a float32 record is filtered in float64 and stored in float32, then
+    imputed and normalised in float32 (other dtypes are imaged as float64); device tensors stay on the
+    device.  With return_indices, also the (empty, noisy) trace indices imputed."""
     if method not in ("surface_wave", "xcorr"):
         raise AssertionError("method must be 'surface_wave' or 'xcorr'")
     on_device = isinstance(data, torch.Tensor) and data.is_cuda
     if on_device:
         t = data.clone()
     else:
-        host = np.asarray(data.detach().cpu() if isinstance(data, torch.Tensor) else data, dtype=np.float64)
-        t = torch.from_numpy(np.array(host, copy=True)).to(default_device())
+        host = np.asarray(data.detach().cpu() if isinstance(data, torch.Tensor) else data)
+        dt_keep = np.float32 if host.dtype == np.float32 else np.float64
+        t = torch.from_numpy(np.array(host, dtype=dt_keep, copy=True)).to(default_device())
     if t.dim() != 2:
         raise ValueError("data must be [n_ch, n_t]")
     bandpass_inplace(t, dt, flo, fhi)

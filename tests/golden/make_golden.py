@@ -336,6 +336,13 @@ def gen_prep(ref):
         bp = d.copy()
         ref.ut.bandpass_data(bp, dt, 1.2, 30)
         out[name + "_idx"] = np.array([ref.ut.find_noise_idx(bp, 5, empty_tr=True)])
+        # a float32 record: data.copy() keeps float32, so the filter output is stored in float32 and the
+        # imputation and the norm run in float32
+        obj = types.SimpleNamespace(method="surface_wave", data=d.astype(np.float32), dt=dt,
+                                    surface_wave_preprecessing_dict=None)
+        tli.TimeLapseImaging._preprocessing_for_surface_waves(obj)
+        assert obj.data_for_imaging.dtype == np.float32
+        out[name + "_surface_wave_f32"] = obj.data_for_imaging
     return out
 
 

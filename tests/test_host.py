@@ -265,3 +265,52 @@ def test_algorithmic_bytes_union_matches_loop():
                 covered[a:a + c] = True
             piv += 4 * int(covered.sum())
         assert seg_algorithmic_bytes(seg, w, hop, sides, 2) == 4 * int(cov.sum()) + piv + 4 * 2 * w
+
+
+def test_ridge_npz_writer(tmp_path):
+    """save_ridge_npz: the notebook's data/<x0>_speeds.npz keys (imaging_diff_speed.ipynb#cell27), pickle-free
+    by default, or the ragged object-array layout the notebook itself writes."""
+    from das_diff_veh_amd.bootstrap import load_ridge_npz, save_ridge_npz
+    fq = np.arange(0.8, 25, 0.1)
+    rv = [[np.arange(116.0) + i for i in range(4)], [np.arange(50.0) - i for i in range(4)]]
+    p = tmp_path / "700_speeds.npz"
+    save_ridge_npz(p, fq, [2.5, 10], [14, 15], fast=rv, slow=rv)
+    f, lb, ub, r = load_ridge_npz(p)
+    assert np.array_equal(f, fq) and list(lb) == [2.5, 10] and list(ub) == [14, 15]
+    assert set(r) == {"fast", "slow"} and r["fast"][0].shape == (4, 116) and r["fast"][1].shape == (4, 50)
+    assert np.array_equal(r["slow"][1][3], rv[1][3])
+    q = tmp_path / "700_ref_layout.npz"
+    save_ridge_npz(q, fq, [2.5, 10], [14, 15], reference_layout=True, fast=rv)
+    with np.load(q, allow_pickle=False) as z:
+        assert set(z.files) == {"freqs", "freq_lb", "freq_ub", "vels_fast"}
+        with pytest.raises(ValueError):  # the object array needs the notebook's allow_pickle=True
+            z["vels_fast"]
+
+
+def _failing_windows():
+    """Golden passes 0 and 3 plus three that cannot be imaged: a one-point trajectory, a gather geometry
+    the pivot falls outside of, and dt = 0.004 (the reference's window-length ValueError)."""
+    import copy
+
+    from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+    g = gio.load("vsg_w500")
+    wins = [SurfaceWaveWindow(**gio.pass_arrays(g, i)) for i in range(5)]
+    trk = copy.copy(wins[1])
+    trk.veh_state_x, trk.veh_state_t = trk.veh_state_x[:1], trk.veh_state_t[:1]
+    geo = copy.copy(wins[2])
+    geo.x_axis = wins[2].x_axis + 1000.0
+    d4 = copy.copy(wins[4])
+    d4.t_axis = np.arange(wins[4].t_axis.size) * 0.004
+    return [wins[0], trk, geo, d4, wins[3]], g
+
+
+def test_pass_failures_skip_and_count():
+    """a failure status per pass (skip + count), decided on the host before any launch."""
+    from das_diff_veh_amd.engine import pass_failures
+    from das_diff_veh_amd.plan import VsgParams
+    wins, _ = _failing_windows()
+    prm = VsgParams(pivot=700, start_x=500, end_x=900, include_other_side=True, norm=False)
+    failed, axes = pass_failures(wins, prm)
+    assert sorted(failed) == [1, 2, 3], failed
+    assert "trajectory" in failed[1] and "geometry" in failed[2] and "broadcast" in failed[3]
+    assert axes[0] is not None and axes[4] is not None and axes[1] is None

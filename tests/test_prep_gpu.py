@@ -35,3 +35,17 @@ def test_preprocessing_device_tensor_float32(device):
     assert got.is_cuda and got.dtype == torch.float32
     ref = g["dead_surface_wave"]
     assert np.abs(got.double().cpu().numpy() - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_float32_record_keeps_its_dtype(device, case):
+    """A float32 host record: the reference's data.copy() stays float32 (filter output stored in float32,
+    imputation and norm in float32); so does ours, against the reference's float32 run (prep.npz)."""
+    from das_diff_veh_amd.preprocess import surface_wave_preprocessing
+    g = gio.load("prep")
+    x = g[case + "_in"]
+    assert x.dtype == np.float32
+    got = surface_wave_preprocessing(x, float(g["dt"]))
+    ref = g[case + "_surface_wave_f32"]
+    assert got.dtype == np.float32 and got.shape == ref.shape
+    assert np.abs(got.astype(np.float64) - ref).max() <= 2e-6 * np.abs(ref).max(), case

@@ -92,3 +92,46 @@ def test_sliding_class_stacks(device):
         checked += 1
     empty = np.setdiff1d(np.arange(n_slot), slots)
     assert np.all(got[empty] == 0.0) and checked >= 4
+
+
+def test_sliding_at_scale_flattened_offsets(device):
+    """configs[3] geometry at scale: 72 windows x 4096 channels x 8192 samples as ONE flattened
+    [72 * 4096, 8192] record, so the units' q * C row offsets pass 2^18 (up to 71 * 4096 = 290,816);
+    trajectories as the sliding bench draws them (crossing uniform along the fiber, 15-30 m/s).
+    Units of the first two and the last four windows are checked against the oracle."""
+    import torch
+
+    from das_diff_veh_amd import vsg
+    from das_diff_veh_amd.plan import UnitPlan, VsgParams
+    from das_diff_veh_amd.synth import TRACK_DT, synth_batch_device
+    n, C, T = 72, 4096, 8192
+    w, x, t, _, _ = synth_batch_device(n, n_ch=C, n_t=T, pivot=C * 8.16 / 2, seed=21, device=device, x_first=0.37,
+                                       track_half=10, chunk=2)
+    rng = np.random.default_rng(5)
+    trk = []
+    for xa, va, ta in zip(rng.uniform(x[32], x[-32], n), rng.uniform(15.0, 30.0, n),
+                          t[T // 2] + rng.uniform(-1.0, 1.0, n)):
+        xs = np.arange(np.floor(xa) - 800.0, np.floor(xa) + 801.0)
+        trk.append((xs, np.round((ta + (xs - xa) / va) / TRACK_DT) * TRACK_DT))
+    kw = dict(include_other_side=True, norm=False)
+    pch = np.arange(32, C - 32, 8)
+    plan = UnitPlan.sliding(x, t, trk, pch, 200.0, VsgParams(**kw))
+    assert int(plan.pass_tab[:, 1].max()) > 2 ** 18
+    flat = vsg.flat_units(w, plan)
+    sc = vsg.vsg_scales(flat, plan, win_sumsq=vsg.unit_sumsq(vsg.window_sumsq(w), plan))
+    got = vsg.vsg_gathers(flat, plan, sc)
+    check = np.flatnonzero((plan.unit_window < 2) | (plan.unit_window >= n - 4))
+    assert check.size >= 6 and int(plan.unit_window[check].max()) == n - 1
+    hosts = {}
+    for u in check:
+        q = int(plan.unit_window[u])
+        if q not in hosts:
+            hosts[q] = w[q].double().cpu().numpy()
+        j = int(plan.unit_pivot[u])
+        p = float(x[plan.pivots[j]])
+        from oracle import vsg as ovsg
+        o = dict(data=hosts[q], x_axis=x, t_axis=t, veh_state_x=trk[q][0], veh_state_t=trk[q][1])
+        ref = ovsg.virtual_shot_gather(o, pivot=p, start_x=p - 200.0, end_x=p + 200.0, wlen=2, **kw)[0]
+        assert gio.gather_rel_err(got[u].double().cpu().numpy(), ref) < TOL, (u, q, j)
+    del w, flat, got
+    torch.cuda.empty_cache()

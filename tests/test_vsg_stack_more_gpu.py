@@ -90,3 +90,21 @@ def test_stack_invalid_windows(device):
     got = vsg.vsg_stack(data, plan, vsg.StackSchedule(np.zeros(plan.n_pass, np.int64), 1, chunk=2))
     with np.errstate(all="ignore"):
         assert gio.gather_rel_err(got.double().cpu().numpy()[0], ovsg.stack(refs)) < TOL
+
+
+def test_skip_failed_passes_stack_the_rest(device):
+    """get_images(skip_failed=True): the broken passes are reported, the class mean is that of the
+    imaged passes (golden gathers 0 and 3), and without the flag the list raises like the reference."""
+    from das_diff_veh_amd.apis.imaging_classes import VirtualShotGathersFromWindows
+    from oracle import vsg as ovsg
+    from tests.test_host import _failing_windows
+    wins, g = _failing_windows()
+    imgs = VirtualShotGathersFromWindows(wins)
+    imgs.get_images(include_other_side=True, pivot=700, start_x=500, end_x=900, wlen=2, skip_failed=True)
+    assert sorted(imgs.failed) == [1, 2, 3]
+    ref = ovsg.stack([g["xcf"][0], g["xcf"][3]])
+    assert gio.gather_rel_err(imgs.avg_image.XCF_out, ref) < 1e-4
+    assert len(imgs.images) == 2
+    with pytest.raises(ValueError):
+        VirtualShotGathersFromWindows(wins).get_images(include_other_side=True, pivot=700, start_x=500, end_x=900,
+                                                       wlen=2)
