@@ -558,11 +558,66 @@ __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int n
   return m;
 }
 
-// rows [c0, c1) of a window (n_t samples each): max |x| bit pattern over the wave
-__device__ __forceinline__ uint32_t scan_rows(const float* __restrict__ base, int64_t ch_stride, int c0, int c1,
-                                              int n_t, bool vec, int lane) {
+// LDS-DMA scan: 1 KiB pieces (one global_load_lds_dwordx4 per wave) land in a ring of RING pieces of this
+// wave's LDS without passing through VGPRs, so a scan wave keeps RING KiB in flight beside its register
+// loads at no register cost.  Written with the M0 recipe of cdna_hip_programming.md (the compiler does
+// not count these loads: the waits below are explicit).
+#ifndef DVH_SCAN_RING
+#define DVH_SCAN_RING 0  // KiB of LDS ring per dedicated scan wave (0: register loads only; 8 / 16 measured
+                         // 12-17 % slower on synth10k: the faster scan lengthens the correlation waves' load latency)
+#endif
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  // lgkmcnt(0) first: the wave's read of the slot this piece overwrites has returned
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// max |x| bit pattern over nf4 consecutive float4 (16-byte aligned) through the LDS ring `ring`
+// (RING KiB, wave-private).  Lanes past the end re-read the last float4: a duplicate leaves the max as is.
+typedef __attribute__((address_space(3))) char lds_char;
+template <int RING>
+__device__ __forceinline__ uint32_t scan_span_ring(const float* __restrict__ q, int nf4, int lane, char* ring_) {
+  const int np = (nf4 + 63) >> 6;
+  // the ring as an LDS (address space 3) pointer: ds_read for the pieces (a flat read would count on vmcnt
+  // and its wait would drain the ring) and the LDS byte offset M0 takes
+  lds_char* ring = (lds_char*)ring_;
+  const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(ring));
+  auto issue = [&](int piece, int slot) {
+    const int i = min(piece * 64 + lane, nf4 - 1);
+    glds16(q + 4 * (int64_t)i, base + (uint32_t)slot * 1024u);
+  };
+  const int pre = np < RING ? np : RING;
+  for (int k = 0; k < pre; ++k) issue(k, k);
   uint32_t m = 0;
-  if (vec && ch_stride == n_t) {  // the unit's rows are one contiguous span
+  int slot = 0;
+  for (int k = 0; k < np; ++k) {
+    if (np - k >= RING) wait_vm<RING - 1>();  // piece k has landed (RING - 1 younger ones in flight)
+    else wait_vm<0>();
+    const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(ring + slot * 1024 + lane * 16) &
+                    0x7fffffffu;
+    m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+    if (k + RING < np) issue(k + RING, slot);
+    slot = slot + 1 == RING ? 0 : slot + 1;
+  }
+  return m;
+}
+
+// rows [c0, c1) of a window (n_t samples each): max |x| bit pattern over the wave; ring (nullable):
+// this wave's LDS-DMA ring of `ring_kib` pieces (16 or 8 KiB)
+__device__ __forceinline__ uint32_t scan_rows(const float* __restrict__ base, int64_t ch_stride, int c0, int c1,
+                                              int n_t, bool vec, int lane, char* ring = nullptr, int ring_kib = 0) {
+  uint32_t m = 0;
+  if (vec && ch_stride == n_t && ring) {  // contiguous rows through the LDS ring
+    const float* q = base + (int64_t)c0 * ch_stride;
+    const int nf4 = ((c1 - c0) * n_t) >> 2;
+    m = ring_kib >= 16 ? scan_span_ring<16>(q, nf4, lane, ring) : scan_span_ring<8>(q, nf4, lane, ring);
+  } else if (vec && ch_stride == n_t) {  // the unit's rows are one contiguous span
     m = scan_span(base + (int64_t)c0 * ch_stride, ((c1 - c0) * n_t) >> 2, lane);
   } else if (vec) {
     for (int c = c0; c < c1; ++c) m = max(m, scan_span(base + (int64_t)c * ch_stride, n_t >> 2, lane));
@@ -663,7 +718,8 @@ __device__ __forceinline__ uint32_t scan_unit_blocks(const VsgArgs& A, int p, in
 // Pull scan units (pass, kScanRows channel rows) until none is left; atomicMax into vflag[pass].
 // list: this wave's LDS scratch of kScanListBytes.
 __device__ __forceinline__ void scan_units(const VsgArgs& A, int n_ch, int n_t, uint32_t* __restrict__ vflag,
-                                           uint32_t* __restrict__ counter, uint32_t* __restrict__ list, int lane) {
+                                           uint32_t* __restrict__ counter, uint32_t* __restrict__ list, int lane,
+                                           char* ring = nullptr, int ring_kib = 0) {
   const int upp = (n_ch + kScanRows - 1) / kScanRows;  // units per pass
   const int n_units = A.n_pass * upp;
   const bool vec = (n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
@@ -677,7 +733,8 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, int n_ch, int n_t, 
     const int p = u / upp, c0 = (u - p * upp) * kScanRows;
     const int c1 = min(c0 + kScanRows, n_ch);
     const uint32_t m = blocks ? scan_unit_blocks(A, p, c0, c1, n_ch, n_t, list, lane)
-                              : scan_rows(A.win + (int64_t)p * A.pass_stride, A.ch_stride, c0, c1, n_t, vec, lane);
+                              : scan_rows(A.win + (int64_t)p * A.pass_stride, A.ch_stride, c0, c1, n_t, vec, lane,
+                                          ring, ring_kib);
     if (lane == 0) atomicMax(vflag + p, m);
     u = un;
   }
@@ -693,15 +750,25 @@ __global__ __launch_bounds__(64 * (kFft + kScan), 4) void vsg_stackv_kernel(
   E eng = make_engine<E>(lds);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint32_t* list;
+  char* ring = nullptr;
+  int ring_kib = 0;
   if (wave < kFft) {
     stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
                     (int64_t)gridDim.x * kFft, DVH_SCAN_COMPLEMENT ? vflag : nullptr);
     list = reinterpret_cast<uint32_t*>(lds + E::kBlockBytes + (size_t)wave * E::kWaveBytes);  // its FFT buffers
+    if (DVH_SCAN_RING && !DVH_SCAN_COMPLEMENT && E::kWaveBytes >= 8192) {  // done correlating: its buffers
+      ring = lds + E::kBlockBytes + (size_t)wave * E::kWaveBytes;
+      ring_kib = 8;
+    }
   } else {
     list = reinterpret_cast<uint32_t*>(lds + E::kBlockBytes + (size_t)kFft * E::kWaveBytes +
                                        (size_t)(wave - kFft) * kScanListBytes);
+    if (DVH_SCAN_RING && !DVH_SCAN_COMPLEMENT) {
+      ring = lds + E::kBlockBytes + (size_t)kFft * E::kWaveBytes + (size_t)(wave - kFft) * DVH_SCAN_RING * 1024;
+      ring_kib = DVH_SCAN_RING;
+    }
   }
-  scan_units(A, n_ch, n_t, vflag, counter, list, lane);
+  scan_units(A, n_ch, n_t, vflag, counter, DVH_SCAN_COMPLEMENT ? list : nullptr, lane, ring, ring_kib);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
@@ -939,7 +1006,9 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
     constexpr int F = DVH_VSTACK_FFT, S = DVH_VSTACK_SCAN;
     const void* fn = (const void*)vsg_stackv_kernel<EngF500, F, S>;
     static_assert(EngF500::kWaveBytes >= kScanListBytes, "a correlation wave's buffers hold its scan list");
-    const size_t lds = EngF500::kBlockBytes + F * EngF500::kWaveBytes + S * kScanListBytes;
+    static_assert(DVH_SCAN_RING == 0 || DVH_SCAN_RING == 8 || DVH_SCAN_RING == 16, "scan ring: 0, 8 or 16 KiB");
+    const size_t scan_lds = DVH_SCAN_COMPLEMENT ? kScanListBytes : (size_t)DVH_SCAN_RING * 1024;
+    const size_t lds = EngF500::kBlockBytes + F * EngF500::kWaveBytes + S * scan_lds;
     const int64_t need = (tasks + F - 1) / F;
     const int grid = (int)(need < 2 * cu_count() ? (need > 0 ? need : 1) : 2 * cu_count());
     void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &n_ch, &n_t, &vflag, &counter};
