@@ -280,7 +280,7 @@ def build_sliding(wl, device, world, rank, scaling, chunk):
     counts = np.bincount(np.concatenate(slot_l), minlength=n_slot)
     if world > 1:
         ct = torch.as_tensor(counts, dtype=torch.int64, device=device)
-        dist.all_reduce(ct)
+        allreduce_stacks([ct])
         counts = ct.cpu().numpy()
     job.batches = []
     for plan, sl in zip(plans, slot_l):
@@ -459,11 +459,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local %= max(1, torch.cuda.device_count())  # identity with one rank per GPU; several ranks share a GPU otherwise
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=device)
+        # RCCL over xGMI, one rank per GPU; DVH_DIST_BACKEND=gloo rehearses the multi-rank step with
+        # several ranks on one GPU (RCCL refuses that), reducing through host copies
+        backend = os.environ.get("DVH_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
 
     job = build(args.workload, device, world, rank, args.scaling, chunk=args.chunk)
     torch.cuda.synchronize()

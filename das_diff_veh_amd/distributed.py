@@ -88,6 +88,8 @@ def sharded_class_means(partial, slots, n_slot, group=None):
 def max_over_ranks(value, device=None, group=None):
     if not dist.is_available() or not dist.is_initialized():
         return value
+    if dist.get_backend(group) == "gloo":
+        device = None  # gloo reduces host tensors
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
