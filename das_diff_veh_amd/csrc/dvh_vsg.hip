@@ -562,6 +562,10 @@ __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int n
 // wave's LDS without passing through VGPRs, so a scan wave keeps RING KiB in flight beside its register
 // loads at no register cost.  Written with the M0 recipe of cdna_hip_programming.md (the compiler does
 // not count these loads: the waits below are explicit).
+#ifndef DVH_CORR_PRIO
+#define DVH_CORR_PRIO 2  // s_setprio of the correlation waves while they correlate (scan waves stay at 0): the
+                         // correlation is the critical path; 1 / 2 / 3 all measured 127.7 k -> 136 k windows/s on synth10k
+#endif
 #ifndef DVH_SCAN_RING
 #define DVH_SCAN_RING 0  // KiB of LDS ring per dedicated scan wave (0: register loads only; 8 / 16 measured
                          // 12-17 % slower on synth10k: the faster scan lengthens the correlation waves' load latency)
@@ -752,10 +756,16 @@ __global__ __launch_bounds__(64 * (kFft + kScan), 4) void vsg_stackv_kernel(
   uint32_t* list;
   char* ring = nullptr;
   int ring_kib = 0;
+#if DVH_CORR_PRIO
+  if (wave < kFft) __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
+#endif
   if (wave < kFft) {
     stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
                     (int64_t)gridDim.x * kFft, DVH_SCAN_COMPLEMENT ? vflag : nullptr);
     list = reinterpret_cast<uint32_t*>(lds + E::kBlockBytes + (size_t)wave * E::kWaveBytes);  // its FFT buffers
+#if DVH_CORR_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if (DVH_SCAN_RING && !DVH_SCAN_COMPLEMENT && E::kWaveBytes >= 8192) {  // done correlating: its buffers
       ring = lds + E::kBlockBytes + (size_t)wave * E::kWaveBytes;
       ring_kib = 8;

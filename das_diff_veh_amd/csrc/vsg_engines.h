@@ -32,6 +32,18 @@
 
 namespace dvh {
 
+#ifndef DVH_RCV_NT
+#define DVH_RCV_NT 0  // 1: receiver samples (read once per (pass, row)) loaded non-temporal, sparing the L2 lines
+                      // of the pivot channel every row of a chunk re-reads
+#endif
+__device__ __forceinline__ float rcv_load(const float* p) {
+#if DVH_RCV_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 enum : int32_t {
   kFlagOtherSide = 1,
   kFlagNorm = 2,
@@ -281,7 +293,7 @@ struct EngF500 {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int n = a + i + 125 * u;
-        z[4 * r + u] = (i < 125) ? make_float2(t.piv[n], t.rcv[n]) : make_float2(0.f, 0.f);
+        z[4 * r + u] = (i < 125) ? make_float2(t.piv[n], rcv_load(t.rcv + n)) : make_float2(0.f, 0.f);
       }
     }
   }
