@@ -74,7 +74,7 @@ WORKLOADS = {
                    n_ch=60, n_t=5500, gen_chunk=64, track_half=350,
                    desc="configs[0]-shape: 700_speeds, fast/mid/slow 330/1442/336, 60 ch x 5500"),
     "sliding": dict(kind="sliding", config="configs[3]", n_total=12544, n_ch=4096, n_t=8192, pool=256, pivot_every=8,
-                    half_aperture=200.0, gen_chunk=2,
+                    half_aperture=200.0, gen_chunk=2, merge=49,
                     desc="configs[3]: synthetic passes x 4096 ch x 8192, sliding pivots every 8 channels (+-200 m, "
                          "49 rows), each pass imaged at every pivot it crosses inside its window; 12,544 passes per "
                          "GPU (100k over 8) as 49 batches over a resident pool of 256 windows; speed classes x "
@@ -282,8 +282,14 @@ def build_sliding(wl, device, world, rank, scaling, chunk):
         ct = torch.as_tensor(counts, dtype=torch.int64, device=device)
         allreduce_stacks([ct])
         counts = ct.cpu().numpy()
+    # batches of new trajectories over the same pool merge into launches of `merge` batches each: one
+    # class (x pivot) slot then holds tens of units per launch instead of ~0.4, so a chunk's inverse
+    # transform and stack atomics are shared by up to `chunk` units
+    merge = max(1, int(wl.get("merge", 1)))
     job.batches = []
-    for plan, sl in zip(plans, slot_l):
+    for m0 in range(0, len(plans), merge):
+        plan = UnitPlan.concat(plans[m0:m0 + merge]) if merge > 1 else plans[m0]
+        sl = np.concatenate(slot_l[m0:m0 + merge])
         job.batches.append(Batch(plan, StackSchedule(sl, n_slot, chunk=chunk, counts=counts),
                                  flat_units(job.windows, plan), unit_sumsq(sumsq, plan),
                                  torch.empty((plan.n_pass, 2), dtype=torch.float32, device=device),
@@ -451,6 +457,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--chunk", type=int, default=8, help="passes per stack task (one wave, one gather row)")
+    ap.add_argument("--sliding-merge", type=int, default=None,
+                    help="sliding: batches of trajectories per stack launch (default: all 49 in one launch)")
     ap.add_argument("--separate-validity", action="store_true",
                     help="window_sumsq launch per batch instead of the validity scan inside the stack launch")
     ap.add_argument("--layout-out", default=None, help="write the launch layout (JSON) for tools/pmc_summary.py")
@@ -469,6 +477,8 @@ def main():
         backend = os.environ.get("DVH_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
 
+    if args.sliding_merge is not None:
+        WORKLOADS["sliding"]["merge"] = args.sliding_merge
     job = build(args.workload, device, world, rank, args.scaling, chunk=args.chunk)
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: {job.windows.shape[0]} resident windows generated in {job.t_gen:.2f}s, host setup "

@@ -32,6 +32,9 @@
 
 namespace dvh {
 
+#ifndef DVH_XPASS_PF
+#define DVH_XPASS_PF 0  // EngF500: prefetch the next task's first sub-window during the last transform of a call
+#endif
 #ifndef DVH_RCV_NT
 #define DVH_RCV_NT 0  // 1: receiver samples (read once per (pass, row)) loaded non-temporal, sparing the L2 lines
                       // of the pivot channel every row of a chunk re-reads
@@ -387,10 +390,15 @@ struct EngF500 {
   // Sub-window q's pivot and receiver samples are loaded one sub-window ahead; with
   // DVH_RCV_AHEAD == 2 the receiver samples (the HBM-missing stream: pivot slices are shared by the
   // chunk's rows and mostly hit L2) two sub-windows ahead, for more latency tolerance when the
-  // launch also streams whole windows (vsg_stackv_kernel).
-  __device__ void spectra(const RowTask& t, const RowTask&, bool, int, int hop, float2 (&Cf)[NH], float2 (&Co)[NH]) {
+  // launch also streams whole windows (vsg_stackv_kernel).  With DVH_XPASS_PF the last sub-window of a
+  // call loads the FIRST sub-window of the caller's next task (tn) into zc, so the first transform of
+  // every pass is prefetched too; a call whose task is not the one prefetched loads its own.
+  float2 zc[8];
+  const float* pre_rcv = nullptr;
+  int pre_a = -1;
+  __device__ void spectra(const RowTask& t, const RowTask& tn, bool has_next, int, int hop, float2 (&Cf)[NH],
+                          float2 (&Co)[NH]) {
     const int nq = t.nwin_f + t.nwin_o;
-    float2 z[8];
 #pragma unroll
     for (int j = 0; j < NH; ++j) {
       Cf[j] = make_float2(0.f, 0.f);
@@ -398,7 +406,15 @@ struct EngF500 {
     }
     live_f = live_o = false;
     auto start = [&](int q) { return q < t.nwin_f ? t.a_f + q * hop : t.a_o + (q - t.nwin_f) * hop; };
-    if (nq > 0) load(t, start(0), z);
+#if DVH_XPASS_PF
+    const int nqn = has_next ? tn.nwin_f + tn.nwin_o : 0;
+    const int an = tn.nwin_f > 0 ? tn.a_f : tn.a_o;
+    if (nq > 0 && !(pre_rcv == t.rcv && pre_a == start(0))) load(t, start(0), zc);
+    pre_rcv = nullptr;
+#else
+    if (nq > 0) load(t, start(0), zc);
+#endif
+    float2 (&z)[8] = zc;
 #if DVH_RCV_AHEAD == 2
     float zr[8];
     if (nq > 1) load_rcv(t, start(1), zr);
@@ -424,6 +440,13 @@ struct EngF500 {
         load(t, start(q + 1), z);
 #endif
       }
+#if DVH_XPASS_PF
+      else if (nqn > 0) {  // the next task's first sub-window, under this one's stages 2-4
+        load(tn, an, z);
+        pre_rcv = tn.rcv;
+        pre_a = an;
+      }
+#endif
       if (!live) continue;  // exactly zero in the reference
       if (q < t.nwin_f) {
         live_f = true;
@@ -433,6 +456,13 @@ struct EngF500 {
         finish(Co);
       }
     }
+#if DVH_XPASS_PF
+    if (nq == 0 && nqn > 0) {
+      load(tn, an, z);
+      pre_rcv = tn.rcv;
+      pre_a = an;
+    }
+#endif
   }
 
   __device__ const float2* inverse(const float2 (&Cf)[NH], const float2 (&Co)[NH]) {

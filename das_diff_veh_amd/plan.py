@@ -467,6 +467,7 @@ class UnitPlan(VsgPlan):
 
     def __init__(self, seg_tab, unit_window, unit_pivot, spatial, prm: VsgParams, n_win, n_ch, n_t, dt, piv_ch=None):
         pivot_idx, start_idx, end_idx, piv = spatial
+        self.spatial, self.dt = spatial, dt
         self.R = int(end_idx[0] - start_idx[0])
         self.w = int(prm.wlen / dt)
         self.hop = int(self.w * (1 - 0.5))
@@ -493,6 +494,22 @@ class UnitPlan(VsgPlan):
                              f"{n_t} samples")
         self.geoms = None
         self._dev = {}
+
+    @classmethod
+    def concat(cls, plans):
+        """One launch over the units of several plans on the SAME windows and pivots (e.g. batches of new
+        trajectories over one resident pool): their tables concatenated.  More units per launch means
+        more passes per (class, pivot) slot chunk, i.e. fewer inverse transforms and stack atomics."""
+        p0 = plans[0]
+        for p in plans[1:]:
+            if (p.n_win, p.win_ch, p.n_t, p.R, p.w, p.hop, p.flags) != (p0.n_win, p0.win_ch, p0.n_t, p0.R, p0.w, p0.hop,
+                                                                         p0.flags):
+                raise ValueError("plans of one launch must share windows, gather shape and flags")
+            if not all(np.array_equal(a, b) for a, b in zip(p.spatial, p0.spatial)):
+                raise ValueError("plans of one launch must share their pivots")
+        return cls(np.concatenate([p.seg_tab for p in plans]), np.concatenate([p.unit_window for p in plans]),
+                   np.concatenate([p.unit_pivot for p in plans]), p0.spatial, p0.prm, p0.n_win, p0.win_ch, p0.n_t,
+                   p0.dt, p0.pivots)
 
     @classmethod
     def sliding(cls, x_axis, t_axis, trajectories, pivot_ch, half_aperture, prm: VsgParams, full_only=True):

@@ -84,3 +84,38 @@ def test_synth10k_job(device):
     x = cs["x_axis"]
     dt = cs["t_axis"][1] - cs["t_axis"][0]
     _check(job, refs, x[0:1023] - x[512], (np.arange(500) - 250) * dt)
+
+
+def test_synth10k_full_job_properties(device):
+    """The bench's synth10k job at its FULL size (BASELINE configs[2]: 10 240 passes of 1 024 x 8 192 as
+    20 batches of 512 over the window pool), through size-independent properties:
+      * the validated launch (correlation + class stack + validity of every window sample in one launch)
+        equals the separate path (dvh_window_sumsq launch, then the plain stack launch) to 1e-5;
+      * stacking is linear: the step's class stacks equal the count-weighted sum of the 20 batches'
+        own class means;
+      * every class image is finite and a step is reproducible to fp32 atomic-order rounding."""
+    import torch
+
+    import bench
+    job = bench.build("synth10k", device, 1, 0)
+    assert len(job.batches) == 20 and sum(b.plan.n_pass for b in job.batches) == 10240
+    bench.step(job, 1, fused=True)
+    fused, fv = job.stack.clone(), job.fv.clone()
+    bench.step(job, 1, fused=False)
+    sep = job.stack.clone()
+    scale = float(sep.abs().max())
+    assert float((fused - sep).abs().max()) <= 1e-5 * scale
+    assert torch.isfinite(fv).all() and torch.isfinite(fused).all()
+    # linearity: per-batch class means (batch-local counts), weighted by the batch's share of each class
+    from das_diff_veh_amd.vsg import StackSchedule, vsg_scales, vsg_stack_validated
+    total = torch.zeros_like(fused)
+    counts = np.bincount(np.concatenate([b.slots for b in job.batches]), minlength=3)
+    for b in job.batches:
+        b.plan.derive()
+        sc = vsg_scales(b.win, b.plan, validity=False)
+        local = np.bincount(b.slots, minlength=3)
+        part = vsg_stack_validated(b.win, b.plan, StackSchedule(b.slots, 3, chunk=8), scales=sc)
+        total += part * torch.as_tensor(local / counts, dtype=torch.float32, device=device)[:, None, None]
+    assert float((total - fused).abs().max()) <= 1e-5 * scale
+    bench.step(job, 1, fused=True)
+    assert float((job.stack - fused).abs().max()) <= 1e-5 * scale

@@ -314,3 +314,30 @@ def test_pass_failures_skip_and_count():
     assert sorted(failed) == [1, 2, 3], failed
     assert "trajectory" in failed[1] and "geometry" in failed[2] and "broadcast" in failed[3]
     assert axes[0] is not None and axes[4] is not None and axes[1] is None
+
+
+def test_unit_plan_concat():
+    """UnitPlan.concat: one launch's tables over several trajectory batches on the same windows."""
+    from das_diff_veh_amd.plan import UnitPlan, VsgParams
+    x = 0.37 * 8.16 + 8.16 * np.arange(300)
+    t = 0.003999999999997783 * np.arange(8192)
+    rng = np.random.default_rng(3)
+
+    def trks(n):
+        out = []
+        for xa, va in zip(rng.uniform(x[40], x[-40], n), rng.uniform(15, 30, n)):
+            xs = np.arange(np.floor(xa) - 800.0, np.floor(xa) + 801.0)
+            out.append((xs, np.round((t[4096] + (xs - xa) / va) / 0.02) * 0.02))
+        return out
+    prm = VsgParams(wlen=2, norm=False, include_other_side=True)
+    pch = np.arange(32, 268, 8)
+    a = UnitPlan.sliding(x, t, trks(3), pch, 200.0, prm)
+    b = UnitPlan.sliding(x, t, trks(3), pch, 200.0, prm)
+    c = UnitPlan.concat([a, b])
+    assert c.n_pass == a.n_pass + b.n_pass
+    assert np.array_equal(c.seg_tab, np.concatenate([a.seg_tab, b.seg_tab]))
+    assert np.array_equal(c.pass_tab, np.concatenate([a.pass_tab, b.pass_tab]))
+    assert np.array_equal(c.unit_window, np.concatenate([a.unit_window, b.unit_window]))
+    other = UnitPlan.sliding(x, t, trks(2), pch[:-1], 200.0, prm)
+    with pytest.raises(ValueError):
+        UnitPlan.concat([a, other])

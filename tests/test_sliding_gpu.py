@@ -135,3 +135,33 @@ def test_sliding_at_scale_flattened_offsets(device):
         assert gio.gather_rel_err(got[u].double().cpu().numpy(), ref) < TOL, (u, q, j)
     del w, flat, got
     torch.cuda.empty_cache()
+
+
+def test_sliding_merged_batches(device):
+    """Two batches of trajectories over the same windows merged into ONE launch (UnitPlan.concat, the
+    sliding bench's layout): every (class, pivot) stack equals the oracle's mean over both batches' units."""
+    from das_diff_veh_amd import vsg
+    from das_diff_veh_amd.plan import UnitPlan, VsgParams
+    from das_diff_veh_amd.synth import synth_batch_device
+    from oracle import vsg as ovsg
+    w, x, t, trk = _case(device, n=3, seed=14)
+    _, _, _, trk2, _ = synth_batch_device(3, n_ch=300, n_t=8192, pivot=1100.0, seed=15, device=device,
+                                          x_first=0.37, track_half=1500, chunk=1)
+    kw = dict(include_other_side=True, norm=False)
+    pch = np.arange(32, w.shape[1] - 32, 8)
+    p1 = UnitPlan.sliding(x, t, trk, pch, 200.0, VsgParams(**kw))
+    p2 = UnitPlan.sliding(x, t, trk2, pch, 200.0, VsgParams(**kw))
+    plan = UnitPlan.concat([p1, p2])
+    assert plan.n_pass == p1.n_pass + p2.n_pass
+    assert np.array_equal(plan.pass_tab, np.concatenate([p1.pass_tab, p2.pass_tab]))
+    slots = np.concatenate([p1.unit_pivot, p2.unit_pivot])  # one class: slot = pivot
+    got = vsg.vsg_stack(vsg.flat_units(w, plan), plan, vsg.StackSchedule(slots, len(pch), chunk=8),
+                        win_sumsq=vsg.unit_sumsq(vsg.window_sumsq(w), plan)).double().cpu().numpy()
+    host = w.double().cpu().numpy()
+    refs = {}
+    for pl, tr in ((p1, trk), (p2, trk2)):
+        for u in range(pl.n_pass):
+            refs.setdefault(int(pl.unit_pivot[u]), []).append(_oracle_unit(host, x, t, tr, pl, u, kw))
+    for j, gs in refs.items():
+        assert gio.gather_rel_err(got[j], ovsg.stack(gs)) < TOL, j
+    assert len(refs) >= 2
