@@ -417,7 +417,11 @@ __global__ __launch_bounds__(kFvThreads) void fv_batch_kernel(
 // the 25 samples the right-edge fit reads), so the Savitzky-Golay pass of its outputs is local.
 // Only the FK columns the tile's frequencies touch are staged per image.
 constexpr int kTileThreads = 256;
+#ifndef DVH_FV_TILE_VT
+#define DVH_FV_TILE_VT 4  // velocities per fv_tile block (4 or 8): more outputs per barrier pair, more registers
+#endif
 
+template <int VT>
 __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
     const double* __restrict__ FK, int32_t B, int32_t G, int32_t n_kb, int32_t n_fb,
     const double* __restrict__ kgrid, double kmin, double kmax, const double* __restrict__ kq, int32_t nF,
@@ -430,7 +434,7 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
   const int half = sgl / 2;
   const int s0 = max(0, f_lo - kSgPad);
   const int s1 = min(nF, max(f_hi + kSgPad, sgl));
-  const int v0 = blockIdx.y * kFvVT;
+  const int v0 = blockIdx.y * VT;
   __shared__ int jr[2];
   if (tid == 0) {
     jr[0] = 1 << 30;
@@ -448,15 +452,15 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
   const int nsub = n_kb * ncol;
   double* fks = smem;                                                 // [n_kb][ncol]
   double* sgs = smem + ((n_kb * n_fb + 1) & ~1);                      // taps + edge fits
-  float* raw = reinterpret_cast<float*>(sgs + ((sgl * sgl + 1) & ~1));  // [kFvVT][S]
+  float* raw = reinterpret_cast<float*>(sgs + ((sgl * sgl + 1) & ~1));  // [VT][S]
   for (int e = tid; e < sgl * sgl; e += kTileThreads) sgs[e] = sg[e];
-  for (int e = tid; e < kFvVT * S; e += kTileThreads) raw[e] = 0.f;
+  for (int e = tid; e < VT * S; e += kTileThreads) raw[e] = 0.f;
   const double* h = sgs;
   const double* el = sgs + sgl;
   const double* er = el + half * sgl;
 
-  int base[kFvVT];
-  double hx0[kFvVT], hx1[kFvVT], hy0 = 0.0, hy1 = 0.0;
+  int base[VT];
+  double hx0[VT], hx1[VT], hy0 = 0.0, hy1 = 0.0;
   {
     const double k0 = kgrid[0], inv_dk = 1.0 / (kgrid[1] - kgrid[0]);
     const int j = own ? fj[f] - jlo : 0;
@@ -465,7 +469,7 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
       hy1 = fw[2 * f + 1];
     }
 #pragma unroll
-    for (int i = 0; i < kFvVT; ++i) {
+    for (int i = 0; i < VT; ++i) {
       const int v = v0 + i;
       base[i] = -1;
       hx0[i] = hx1[i] = 0.0;
@@ -497,8 +501,8 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
     const int m = e / ncol;
     goff[q] = e < nsub ? m * n_fb + (e - m * ncol) : -1;
   }
-  const int t_r = tid / nb4, t_f0 = f_lo + (tid - t_r * nb4) * 4;
-  const bool has_task = tid < kFvVT * nb4 && v0 + t_r < nV;
+  // filter tasks (velocity row, 4 outputs): tid and, for VT = 8, tid + kTileThreads
+  constexpr int kTasks = (VT * 64 + kTileThreads - 1) / kTileThreads;  // task slots per thread (nb4 <= 64)
   // Two barriers per image: the next image's FK sub-grid is staged into fks while this image is
   // filtered (fks is free once every thread has sampled), and its first kStage elements come from
   // registers loaded one image earlier, so the FK fetch latency is not exposed between barriers.
@@ -530,7 +534,7 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
     lds_barrier();  // fks holds image it; the previous image's filter is done with raw
     if (own) {
 #pragma unroll
-      for (int i = 0; i < kFvVT; ++i) {
+      for (int i = 0; i < VT; ++i) {
         if (base[i] < 0) continue;
         const int m = base[i];
         const double z00 = fks[m], z01 = fks[m + 1], z10 = fks[m + ncol], z11 = fks[m + ncol + 1];
@@ -543,8 +547,12 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
       stage_img(it + 1);
       if (it + 2 < n_img) load_pre(it + 2);
     }
-    // one task per thread (4 nb4 <= kTileThreads: TO + 2 kSgPad <= kTileThreads)
-    if (has_task) {
+    // VT * nb4 filter tasks over the block's threads (TO + 2 kSgPad <= kTileThreads)
+#pragma unroll
+    for (int ts = 0; ts < kTasks; ++ts) {
+      const int task = tid + ts * kTileThreads;
+      const int t_r = task / nb4, t_f0 = f_lo + (task - t_r * nb4) * 4;
+      if (!(task < VT * nb4 && v0 + t_r < nV)) continue;
       const int r = t_r, f0 = t_f0, v = v0 + r;
       const float* row = raw + r * S + kSgPad - s0;  // row[x] = sample at frequency x
       double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -703,24 +711,25 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
     if (const char* ev = getenv("DVH_FV_TILE")) mode = atoi(ev);  // A/B: 0 = batched / per-image, 2 = always tiled
     const size_t lds_t = sizeof(double) * (size_t)(((size_t)n_kb * n_fb + 1) & ~(size_t)1) +
                          sizeof(double) * (size_t)((sgl * sgl + 1) & ~1) +
-                         sizeof(float) * (size_t)kFvVT * (2 * kSgPad + kTileThreads + 4);
+                         sizeof(float) * (size_t)DVH_FV_TILE_VT * (2 * kSgPad + kTileThreads + 4);
     // large batches of long frequency axes only: on few images (the bench's 3 class stacks of
     // 1 000 x 242) the per-image kernel measured faster (1.100 vs 1.125 ms per bench step), and with
     // tiles under 160 outputs (nF = 242: 2 x 124) half the block idles -- the batched kernel packs
     // 4 velocity groups there (sliding bench 16.2 vs 17.6 ms per step)
-    const int64_t work = (int64_t)B * nt * ((nV + kFvVT - 1) / kFvVT);
+    const int64_t work = (int64_t)B * nt * ((nV + kFvVT - 1) / kFvVT);  // in 4-velocity units
     if (mode && ((work >= 8192 && TO >= 160) || mode > 1) && last >= kSgPad + 1 && TO + 2 * kSgPad <= kTileThreads &&
         nF >= sgl && lds_t <= 64 * 1024) {
-      hipError_t e = hipFuncSetAttribute((const void*)fv_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+      constexpr int VT = DVH_FV_TILE_VT;
+      hipError_t e = hipFuncSetAttribute((const void*)fv_tile_kernel<VT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)lds_t);
       if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
-      const int nvc = (nV + kFvVT - 1) / kFvVT;
+      const int nvc = (nV + VT - 1) / VT;
       const int64_t pairs = (int64_t)nt * nvc;
       int G = (int)((pairs * B + 8191) / 8192);  // ~8 k blocks, at most 64 images each
       G = G < 1 ? 1 : (G > 64 ? 64 : G);
       if (const char* ev = getenv("DVH_FV_TG")) G = atoi(ev) > 0 ? atoi(ev) : G;
       dim3 grid(nt, nvc, (B + G - 1) / G);
-      hipLaunchKernelGGL(fv_tile_kernel, grid, dim3(kTileThreads), lds_t, (hipStream_t)stream, FK, B, G, n_kb, n_fb,
+      hipLaunchKernelGGL(fv_tile_kernel<VT>, grid, dim3(kTileThreads), lds_t, (hipStream_t)stream, FK, B, G, n_kb, n_fb,
                          kgrid, kmin, kmax, kq, nF, nV, TO, fj, fw, sg, sgl, fv);
       return last_launch();
     }

@@ -11,3 +11,8 @@ for m in 49 7 1; do
   summ gpurun_out/n.json "sliding merge $m" | tee -a gpurun_out/n_summary.txt
 done
 VARIANTS="default xpf" bash tools/gpu_r2l.sh
+for v in default vt8; do
+  lib=""; [ $v = default ] || lib=das_diff_veh_amd/lib/variants/$v.so
+  DVH_LIB=$lib timeout -k 10 200 python tools/bench_timelapse.py > gpurun_out/n_tl.json 2> gpurun_out/n_tl.err || { echo "tl $v failed"; tail -5 gpurun_out/n_tl.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/n_tl.json')); print('timelapse $v', round(d['value']), round(d['ms_per_step'],3), {k: round(x['us'],1) for k,x in d['kernels'].items()}, d['parity'])" | tee -a gpurun_out/n_summary.txt
+done
