@@ -421,12 +421,17 @@ constexpr int kTileThreads = 256;
 #define DVH_FV_TILE_VT 4  // velocities per fv_tile block (4 or 8): more outputs per barrier pair, more registers
 #endif
 
-template <int VT>
+// kCells: instead of every FK row of the columns the tile touches, the block stages only the cells its
+// bilinear stencils read (host tables of DispPlan.cell_tables, per (velocity chunk, tile) ct: the cells'
+// FK offsets, column-major, and per (frequency, velocity) the compact indices b0 of (m, j) and b1 of
+// (m, j + 1) and the FITPACK interval m) -- a few rows per column instead of all n_kb.
+template <int VT, bool kCells>
 __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
     const double* __restrict__ FK, int32_t B, int32_t G, int32_t n_kb, int32_t n_fb,
     const double* __restrict__ kgrid, double kmin, double kmax, const double* __restrict__ kq, int32_t nF,
     int32_t nV, int32_t TO, const int32_t* __restrict__ fj, const double* __restrict__ fw,
-    const double* __restrict__ sg, int32_t sgl, float* __restrict__ fv) {
+    const double* __restrict__ sg, int32_t sgl, float* __restrict__ fv, const int32_t* __restrict__ cell_off,
+    const int32_t* __restrict__ n_cell, int32_t max_cell, const int4* __restrict__ qidx) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int S = 2 * kSgPad + kTileThreads + 4;  // row stride (floats), multiple of 4
   const int tid = threadIdx.x;
@@ -435,23 +440,30 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
   const int s0 = max(0, f_lo - kSgPad);
   const int s1 = min(nF, max(f_hi + kSgPad, sgl));
   const int v0 = blockIdx.y * VT;
-  __shared__ int jr[2];
-  if (tid == 0) {
-    jr[0] = 1 << 30;
-    jr[1] = -1;
-  }
-  __syncthreads();
   const int f = s0 + tid;
   const bool own = f < s1;
-  if (own) {
-    atomicMin(&jr[0], fj[f]);
-    atomicMax(&jr[1], fj[f]);
+  const int ct = blockIdx.y * gridDim.x + blockIdx.x;  // (velocity chunk, tile) of the cell tables
+  int jlo = 0, ncol = 0, nsub = 0;
+  if constexpr (kCells) {
+    nsub = n_cell[ct];
+  } else {
+    __shared__ int jr[2];
+    if (tid == 0) {
+      jr[0] = 1 << 30;
+      jr[1] = -1;
+    }
+    __syncthreads();
+    if (own) {
+      atomicMin(&jr[0], fj[f]);
+      atomicMax(&jr[1], fj[f]);
+    }
+    __syncthreads();
+    jlo = jr[0];
+    ncol = jr[1] + 2 - jr[0];  // columns jlo .. jhi + 1
+    nsub = n_kb * ncol;
   }
-  __syncthreads();
-  const int jlo = jr[0], ncol = jr[1] + 2 - jr[0];  // columns jlo .. jhi + 1
-  const int nsub = n_kb * ncol;
-  double* fks = smem;                                                 // [n_kb][ncol]
-  double* sgs = smem + ((n_kb * n_fb + 1) & ~1);                      // taps + edge fits
+  double* fks = smem;  // [n_kb][ncol], or the compact cells
+  double* sgs = smem + (((kCells ? max_cell : n_kb * n_fb) + 1) & ~1);  // taps + edge fits
   float* raw = reinterpret_cast<float*>(sgs + ((sgl * sgl + 1) & ~1));  // [VT][S]
   for (int e = tid; e < sgl * sgl; e += kTileThreads) sgs[e] = sg[e];
   for (int e = tid; e < VT * S; e += kTileThreads) raw[e] = 0.f;
@@ -459,11 +471,11 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
   const double* el = sgs + sgl;
   const double* er = el + half * sgl;
 
-  int base[VT];
+  int base[VT], base1[VT];
   double hx0[VT], hx1[VT], hy0 = 0.0, hy1 = 0.0;
   {
     const double k0 = kgrid[0], inv_dk = 1.0 / (kgrid[1] - kgrid[0]);
-    const int j = own ? fj[f] - jlo : 0;
+    const int j = own && !kCells ? fj[f] - jlo : 0;
     if (own) {
       hy0 = fw[2 * f];
       hy1 = fw[2 * f + 1];
@@ -476,15 +488,24 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
       if (own && v < nV) {
         double q = kq[(int64_t)f * nV + v];
         q = q < kmin ? kmin : (q > kmax ? kmax : q);
-        int m = (int)floor((q - k0) * inv_dk);
-        m = m < 0 ? 0 : (m > n_kb - 2 ? n_kb - 2 : m);
-        while (m < n_kb - 2 && q >= kgrid[m + 1]) ++m;
-        while (m > 0 && q < kgrid[m]) --m;
+        int m;
+        if constexpr (kCells) {
+          const int4 ix = qidx[((int64_t)ct * kTileThreads + tid) * VT + i];
+          m = ix.z;
+          base[i] = ix.x;
+          base1[i] = ix.y;
+        } else {
+          m = (int)floor((q - k0) * inv_dk);
+          m = m < 0 ? 0 : (m > n_kb - 2 ? n_kb - 2 : m);
+          while (m < n_kb - 2 && q >= kgrid[m + 1]) ++m;
+          while (m > 0 && q < kgrid[m]) --m;
+          base[i] = m * ncol + j;
+          base1[i] = base[i] + 1;
+        }
         const double klo = kgrid[m], khi = kgrid[m + 1];
         const double fx = 1.0 / (khi - klo);
         hx0[i] = fx * (khi - q);
         hx1[i] = fx * (q - klo);
-        base[i] = m * ncol + j;
       }
     }
   }
@@ -498,8 +519,12 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 #pragma unroll
   for (int q = 0; q < kStage; ++q) {
     const int e = tid + q * kTileThreads;
-    const int m = e / ncol;
-    goff[q] = e < nsub ? m * n_fb + (e - m * ncol) : -1;
+    if constexpr (kCells) {
+      goff[q] = e < nsub ? cell_off[(int64_t)ct * max_cell + e] : -1;
+    } else {
+      const int m = e / ncol;
+      goff[q] = e < nsub ? m * n_fb + (e - m * ncol) : -1;
+    }
   }
   // filter tasks (velocity row, 4 outputs): tid and, for VT = 8, tid + kTileThreads
   constexpr int kTasks = (VT * 64 + kTileThreads - 1) / kTileThreads;  // task slots per thread (nb4 <= 64)
@@ -514,8 +539,12 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
     for (int q = 0; q < kStage; ++q)
       if (goff[q] >= 0) fks[tid + q * kTileThreads] = pre[q];
     for (int e = tid + kStage * kTileThreads; e < nsub; e += kTileThreads) {
-      const int m = e / ncol, c = e - m * ncol;
-      fks[e] = F[m * n_fb + c];
+      if constexpr (kCells) {
+        fks[e] = F[cell_off[(int64_t)ct * max_cell + e]];
+      } else {
+        const int m = e / ncol, c = e - m * ncol;
+        fks[e] = F[m * n_fb + c];
+      }
     }
   };
   auto load_pre = [&](int it_l) {
@@ -536,8 +565,10 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 #pragma unroll
       for (int i = 0; i < VT; ++i) {
         if (base[i] < 0) continue;
-        const int m = base[i];
-        const double z00 = fks[m], z01 = fks[m + 1], z10 = fks[m + ncol], z11 = fks[m + ncol + 1];
+        // (m, j), (m, j + 1), (m + 1, j), (m + 1, j + 1): row-major sub-grid, or compact column-major cells
+        const int m = base[i], m1 = base1[i];
+        const double z00 = fks[m], z01 = kCells ? fks[m1] : fks[m + 1];
+        const double z10 = kCells ? fks[m + 1] : fks[m + ncol], z11 = kCells ? fks[m1 + 1] : fks[m + ncol + 1];
         raw[i * S + kSgPad + tid] =
             (float)(z00 * hx0[i] * hy0 + z01 * hx0[i] * hy1 + z10 * hx1[i] * hy0 + z11 * hx1[i] * hy1);
       }
@@ -720,7 +751,7 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
     if (mode && ((work >= 8192 && TO >= 160) || mode > 1) && last >= kSgPad + 1 && TO + 2 * kSgPad <= kTileThreads &&
         nF >= sgl && lds_t <= 64 * 1024) {
       constexpr int VT = DVH_FV_TILE_VT;
-      hipError_t e = hipFuncSetAttribute((const void*)fv_tile_kernel<VT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipError_t e = hipFuncSetAttribute((const void*)fv_tile_kernel<VT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)lds_t);
       if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
       const int nvc = (nV + VT - 1) / VT;
@@ -729,8 +760,9 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
       G = G < 1 ? 1 : (G > 64 ? 64 : G);
       if (const char* ev = getenv("DVH_FV_TG")) G = atoi(ev) > 0 ? atoi(ev) : G;
       dim3 grid(nt, nvc, (B + G - 1) / G);
-      hipLaunchKernelGGL(fv_tile_kernel<VT>, grid, dim3(kTileThreads), lds_t, (hipStream_t)stream, FK, B, G, n_kb, n_fb,
-                         kgrid, kmin, kmax, kq, nF, nV, TO, fj, fw, sg, sgl, fv);
+      hipLaunchKernelGGL((fv_tile_kernel<VT, false>), grid, dim3(kTileThreads), lds_t, (hipStream_t)stream, FK, B, G,
+                         n_kb, n_fb, kgrid, kmin, kmax, kq, nF, nV, TO, fj, fw, sg, sgl, fv, nullptr, nullptr, 0,
+                         nullptr);
       return last_launch();
     }
   }
@@ -768,5 +800,43 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
   dim3 grid((nV + kVC - 1) / kVC, B);
   hipLaunchKernelGGL(fv_kernel, grid, dim3(256), lds, (hipStream_t)stream, FK, n_kb, n_fb, kgrid, kmin, kmax, kq, nF,
                      nV, fj, fw, sg, sgl, fv);
+  return last_launch();
+}
+
+DVH_API int dvh_disp_fv_cells(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, const double* kgrid, double kmin,
+                              double kmax, const double* kq, int32_t nF, int32_t nV, const double* fw, const double* sg,
+                              int32_t sgl, int32_t TO, int32_t n_tile, int32_t VT, int32_t max_cell,
+                              const int32_t* cell_off, const int32_t* n_cell, const int32_t* qidx, float* fv,
+                              void* stream) {
+  if (!FK || !kgrid || !kq || !fw || !sg || !fv || !cell_off || !n_cell || !qidx)
+    return set_error(-2, "null pointer argument");
+  if (n_kb < 2 || n_fb < 2) return set_error(-2, "FK grid needs at least 2 x 2 bins");
+  if (sgl != 2 * kSgPad + 1 && (sgl % 2 == 0 || sgl > nF)) return set_error(-4, "savgol window must be odd and <= nF");
+  if (VT != kFvVT) return set_error(-4, "cell tables are built for 4 velocities per block");
+  if (TO <= 0 || TO % 4 || n_tile <= 0 || (int64_t)(n_tile - 1) * TO >= nF || (int64_t)n_tile * TO < nF)
+    return set_error(-2, "tile width / count do not cover the frequencies");
+  if (max_cell <= 0 || max_cell > 8192) return set_error(-4, "cell table wider than 8192 cells");
+  for (int t = 0; t < n_tile; ++t) {  // every tile's sampled span (with its halo) fits the block
+    const int f_lo = t * TO, f_hi = nF < f_lo + TO ? nF : f_lo + TO;
+    const int s0 = f_lo - kSgPad > 0 ? f_lo - kSgPad : 0;
+    const int s1 = nF < (f_hi + kSgPad > sgl ? f_hi + kSgPad : sgl) ? nF : (f_hi + kSgPad > sgl ? f_hi + kSgPad : sgl);
+    if (s1 - s0 > kTileThreads || (f_hi - f_lo + 3) / 4 > 64) return set_error(-4, "tile wider than the block");
+    if (t == n_tile - 1 && f_hi - f_lo < kSgPad + 1 && n_tile > 1) return set_error(-4, "last tile too narrow");
+  }
+  if (B <= 0 || nV <= 0) return 0;
+  const size_t lds = sizeof(double) * (size_t)((max_cell + 1) & ~1) + sizeof(double) * (size_t)((sgl * sgl + 1) & ~1) +
+                     sizeof(float) * (size_t)kFvVT * (2 * kSgPad + kTileThreads + 4);
+  hipError_t e = hipFuncSetAttribute((const void*)fv_tile_kernel<kFvVT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+  const int nvc = (nV + kFvVT - 1) / kFvVT;
+  const int64_t pairs = (int64_t)n_tile * nvc;
+  int G = (int)((pairs * B + 8191) / 8192);  // ~8 k blocks, at most 64 images each
+  G = G < 1 ? 1 : (G > 64 ? 64 : G);
+  if (const char* ev = getenv("DVH_FV_TG")) G = atoi(ev) > 0 ? atoi(ev) : G;
+  dim3 grid(n_tile, nvc, (B + G - 1) / G);
+  hipLaunchKernelGGL((fv_tile_kernel<kFvVT, true>), grid, dim3(kTileThreads), lds, (hipStream_t)stream, FK, B, G, n_kb,
+                     n_fb, kgrid, kmin, kmax, kq, nF, nV, TO, (const int32_t*)nullptr, fw, sg, sgl, fv, cell_off, n_cell,
+                     max_cell, (const int4*)qidx);
   return last_launch();
 }

@@ -12,6 +12,7 @@ Every FLOP on the data runs in the kernels (das_diff_veh_amd/csrc/dvh_disp.hip).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import scipy.signal
@@ -69,6 +70,7 @@ class DispPlan:
         ones = np.ones(self.nV)
         kq = np.stack([np.sort(np.divide(ones * fr, self.vels), kind="mergesort") for fr in self.freqs])
         kqc, m0 = _intervals(fft_k, kq)
+        self._m0 = m0
         if full_grid:
             j_lo, j_hi, m_lo, m_hi = 0, nf - 1, 0, nk - 1
         else:
@@ -110,7 +112,72 @@ class DispPlan:
         h, el, er_ = savgol_operator(sg_window, sg_order)
         self.sgl = sg_window
         self.sg = np.concatenate([h, el.ravel(), er_.ravel()])
+        self.mk = (m0 - m_lo).astype(np.int32)  # FITPACK interval of every (f, v) query, compact-grid rows
+        self._cells = None
         self._dev = {}
+
+    # f-v blocks of the frequency-tiled kernel: 256 threads, 4 velocities, tiles of <= 200 outputs with a
+    # 12-sample halo (one tile when the whole axis fits the block)
+    TILE_THREADS, TILE_VT, TILE_PAD = 256, 4, 12
+
+    def cell_tables(self):
+        """Per (velocity chunk, frequency tile) block of dvh_disp_fv_cells: the FK cells its bilinear stencils
+        read -- rows m, m + 1 of columns j, j + 1 for every (f, v) it samples -- column-major (each column's
+        rows lo..hi contiguous), and per (f, v) the compact indices of (m, j) and (m, j + 1) with m.
+        Returns a dict of numpy tables (cached), or None when a block would not fit."""
+        if self._cells is not None:
+            return self._cells or None
+        T, VT, pad = self.TILE_THREADS, self.TILE_VT, self.TILE_PAD
+        nF, nV = self.nF, self.nV
+        nt = 1 if nF <= T else -(-nF // 200)
+        TO = (-(-nF // nt) + 3) & ~3
+        ok = nF >= self.sgl
+        nvc = -(-nV // VT)
+        n_ct = nvc * nt
+        qidx = np.zeros((n_ct, T, VT, 4), dtype=np.int32)
+        offs, ncell = [], np.zeros(n_ct, dtype=np.int32)
+        for t in range(nt):
+            f_lo, f_hi = t * TO, min(nF, t * TO + TO)
+            s0, s1 = max(0, f_lo - pad), min(nF, max(f_hi + pad, self.sgl))
+            ok &= (s1 - s0 <= T) and (nt == 1 or f_hi - f_lo >= pad + 1)
+            fs = np.arange(s0, s1)
+            for c in range(nvc):
+                vs = np.arange(c * VT, min(nV, c * VT + VT))
+                M = self.mk[np.ix_(fs, vs)].astype(np.int64)
+                J = np.broadcast_to(self.fj[fs].astype(np.int64)[:, None], M.shape)
+                cols = np.concatenate([J.ravel(), J.ravel() + 1])
+                rows = np.concatenate([M.ravel(), M.ravel()])
+                ucol, inv = np.unique(cols, return_inverse=True)
+                lo = np.full(ucol.size, np.iinfo(np.int64).max)
+                hi = np.full(ucol.size, -1)
+                np.minimum.at(lo, inv, rows)
+                np.maximum.at(hi, inv, rows + 1)
+                cnt = hi - lo + 1
+                start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+                col_of = np.repeat(ucol, cnt)
+                row_of = np.arange(cnt.sum()) - np.repeat(start, cnt) + np.repeat(lo, cnt)
+                ct = c * nt + t
+                offs.append((row_of * self.n_fb + col_of).astype(np.int32))
+                ncell[ct] = offs[-1].size
+                c0, c1 = np.searchsorted(ucol, J), np.searchsorted(ucol, J + 1)
+                qidx[ct, :fs.size, :vs.size, 0] = start[c0] + M - lo[c0]
+                qidx[ct, :fs.size, :vs.size, 1] = start[c1] + M - lo[c1]
+                qidx[ct, :fs.size, :vs.size, 2] = M
+        # offs was filled tile-major: reorder to ct = c * nt + t
+        order = [c * nt + t for t in range(nt) for c in range(nvc)]
+        by_ct = [None] * n_ct
+        for k, ct in enumerate(order):
+            by_ct[ct] = offs[k]
+        max_cell = int(ncell.max())
+        ok &= max_cell <= 8192
+        if not ok:
+            self._cells = {}
+            return None
+        cell_off = np.zeros((n_ct, max_cell), dtype=np.int32)
+        for ct, o in enumerate(by_ct):
+            cell_off[ct, :o.size] = o
+        self._cells = dict(TO=TO, n_tile=nt, max_cell=max_cell, cell_off=cell_off, n_cell=ncell, qidx=qidx)
+        return self._cells
 
     def tables(self, device):
         key = str(device)
@@ -155,12 +222,38 @@ def fk_grid(data, plan: DispPlan, norm=False, slots=None, weights=None, n_slot=N
     return FK
 
 
+def _use_cells(plan: DispPlan, B: int) -> bool:
+    """The cell-staged tiled kernel for batches that fill the chip (>= 4 096 blocks); few images (the
+    bench's class stacks) keep the per-image kernel.  DVH_FV_CELLS=0 / 1 forces it off / on (A/B)."""
+    env = os.environ.get("DVH_FV_CELLS")
+    if env is not None:
+        return env != "0" and plan.cell_tables() is not None
+    if "DVH_FV_TILE" in os.environ or "DVH_FV_G" in os.environ:  # A/B of the dvh_disp_fv kernels
+        return False
+    nt = 1 if plan.nF <= DispPlan.TILE_THREADS else -(-plan.nF // 200)
+    if B * nt * -(-plan.nV // DispPlan.TILE_VT) < 4096:
+        return False
+    return plan.cell_tables() is not None
+
+
 def fv_from_fk(FK, plan: DispPlan, out=None):
     dev = FK.device
     tb = plan.tables(dev)
     B = FK.shape[0]
     if out is None:
         out = torch.empty((B, plan.nV, plan.nF), dtype=torch.float32, device=dev)
+    if _use_cells(plan, B):
+        key = ("cells", str(dev))
+        if key not in plan._dev:
+            ct = plan.cell_tables()
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+            plan._dev[key] = dict(ct, cell_off=t(ct["cell_off"]), n_cell=t(ct["n_cell"]), qidx=t(ct["qidx"]))
+        c = plan._dev[key]
+        _lib.call("dvh_disp_fv_cells", _lib.ptr(FK), B, plan.n_kb, plan.n_fb, _lib.ptr(tb["kgrid"]), plan.kmin,
+                  plan.kmax, _lib.ptr(tb["kq"]), plan.nF, plan.nV, _lib.ptr(tb["fw"]), _lib.ptr(tb["sg"]), plan.sgl,
+                  c["TO"], c["n_tile"], DispPlan.TILE_VT, c["max_cell"], _lib.ptr(c["cell_off"]), _lib.ptr(c["n_cell"]),
+                  _lib.ptr(c["qidx"]), _lib.ptr(out), _lib.stream_of(dev))
+        return out
     _lib.call("dvh_disp_fv", _lib.ptr(FK), B, plan.n_kb, plan.n_fb, _lib.ptr(tb["kgrid"]), plan.kmin, plan.kmax,
               _lib.ptr(tb["kq"]), plan.nF, plan.nV, _lib.ptr(tb["fj"]), _lib.ptr(tb["fw"]), _lib.ptr(tb["sg"]),
               plan.sgl, _lib.ptr(out), _lib.stream_of(dev))

@@ -127,6 +127,17 @@ int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, const d
                 double kmax, const double* kq, int32_t nF, int32_t nV, const int32_t* fj, const double* fw,
                 const double* sg, int32_t sgl, float* fv, void* stream);
 
+/* dvh_disp_fv for large batches with the FK cells staged per block: 256-thread blocks of 4 velocities x a
+ * frequency tile (TO outputs, n_tile tiles, 12-sample halos; one tile when nF <= 256), block ct =
+ * chunk * n_tile + tile stages only the cells its bilinear stencils read: cell_off[ct][max_cell] (FK
+ * offsets m * n_fb + j, column-major per column), n_cell[ct], and per (f, v) of the block
+ * qidx[ct][256][4][4] int32 = {compact index of (m, j), of (m, j + 1), m, 0}, f = tile start - halo + thread.
+ * Tables: das_diff_veh_amd.disp.DispPlan.cell_tables.  VT must be 4.  Same outputs as dvh_disp_fv. */
+int dvh_disp_fv_cells(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, const double* kgrid, double kmin,
+                      double kmax, const double* kq, int32_t nF, int32_t nV, const double* fw, const double* sg,
+                      int32_t sgl, int32_t TO, int32_t n_tile, int32_t VT, int32_t max_cell, const int32_t* cell_off,
+                      const int32_t* n_cell, const int32_t* qidx, float* fv, void* stream);
+
 /* ---------------------------------------------------------------- bootstrap / convergence
  * bootstrap_disp (apis/imaging_classes.py:8-48): per-pass gathers once, then per resample the mean
  * stack, its f-v image (dvh_disp_*) and the ridge picks (extract_ridge_ref_idx, modules/utils.py:621-678). */

@@ -10,7 +10,8 @@ TOL = 1e-4
 
 
 @pytest.mark.parametrize("mode", [None, ("DVH_FV_TILE", "2"), ("DVH_FV_TILE", "0"), ("DVH_FV_G", "3"),
-                                  ("DVH_FV_G", "16"), ("DVH_FV_TG", "3"), ("DVH_FV_G", "0")])
+                                  ("DVH_FV_G", "16"), ("DVH_FV_TG", "3"), ("DVH_FV_G", "0"), ("DVH_FV_CELLS", "1"),
+                                  ("DVH_FV_CELLS", "0")])
 @pytest.mark.parametrize("B,nv,nf", [(40, 512, 1000), (7, 300, 242), (5, 64, 1001), (3, 61, 25), (4, 33, 413)])
 def test_fv_batch_vs_oracle(device, monkeypatch, B, nv, nf, mode):
     """mode: kernel selection read at each launch -- None = default dispatch, DVH_FV_TILE=2 -> always
@@ -21,6 +22,8 @@ def test_fv_batch_vs_oracle(device, monkeypatch, B, nv, nf, mode):
             monkeypatch.setenv("DVH_FV_TILE", "0")
         if mode[0] == "DVH_FV_TG":
             monkeypatch.setenv("DVH_FV_TILE", "2")
+        if mode == ("DVH_FV_CELLS", "1"):  # also split the images over several blocks
+            monkeypatch.setenv("DVH_FV_TG", "3")
         monkeypatch.setenv(*mode)
     from das_diff_veh_amd.disp import DispPlan, fv_maps
     from das_diff_veh_amd.synth import synth_gathers

@@ -341,3 +341,41 @@ def test_unit_plan_concat():
     other = UnitPlan.sliding(x, t, trks(2), pch[:-1], 200.0, prm)
     with pytest.raises(ValueError):
         UnitPlan.concat([a, other])
+
+
+@pytest.mark.parametrize("nv,nf", [(1000, 242), (512, 1000)])
+def test_fv_cell_tables_address_every_stencil_cell(nv, nf):
+    """DispPlan.cell_tables (dvh_disp_fv_cells): for every block and every (f, v) it samples, the compact
+    indices reach exactly FK[m, j], FK[m + 1, j], FK[m, j + 1], FK[m + 1, j + 1] of the plan's own FITPACK
+    intervals, through the block's staged cells only."""
+    from das_diff_veh_amd.disp import DispPlan
+    dt = 0.003999999999997783
+    freqs = np.arange(0.8, 25, 0.1) if nf == 242 else np.linspace(1.0, 24.0, nf)
+    vels = np.arange(200, 200 + nv) if nv == 1000 else np.linspace(150.0, 1200.0, nv)
+    plan = DispPlan(25, 500, 8.16, dt, freqs, vels)
+    ct = plan.cell_tables()
+    assert ct is not None
+    T, VT, pad = DispPlan.TILE_THREADS, DispPlan.TILE_VT, DispPlan.TILE_PAD
+    rng = np.random.default_rng(0)
+    FK = rng.standard_normal((plan.n_kb, plan.n_fb))
+    flat = FK.ravel()
+    nt, TO = ct["n_tile"], ct["TO"]
+    nvc = -(-plan.nV // VT)
+    assert ct["cell_off"].shape == (nvc * nt, ct["max_cell"])
+    for c in range(nvc):
+        vs = np.arange(c * VT, min(plan.nV, c * VT + VT))
+        for t in range(nt):
+            k = c * nt + t
+            cells = flat[ct["cell_off"][k, :ct["n_cell"][k]]]
+            f_lo, f_hi = t * TO, min(plan.nF, t * TO + TO)
+            s0, s1 = max(0, f_lo - pad), min(plan.nF, max(f_hi + pad, plan.sgl))
+            assert s1 - s0 <= T
+            q = ct["qidx"][k, :s1 - s0, :vs.size]
+            m = plan.mk[s0:s1, vs]
+            j = plan.fj[s0:s1, None]
+            assert np.array_equal(q[..., 2], m)
+            assert np.array_equal(cells[q[..., 0]], FK[m, j]) and np.array_equal(cells[q[..., 0] + 1], FK[m + 1, j])
+            assert np.array_equal(cells[q[..., 1]], FK[m, j + 1]) and np.array_equal(cells[q[..., 1] + 1], FK[m + 1, j + 1])
+    # the point of the tables: a block stages a few rows per column, not the n_kb rows
+    assert ct["max_cell"] < 0.5 * plan.n_kb * plan.n_fb
+    print("cells per block", int(ct["n_cell"].mean()), "of", plan.n_kb * plan.n_fb)

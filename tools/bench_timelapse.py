@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from das_diff_veh_amd import _lib  # noqa: E402
-from das_diff_veh_amd.disp import DispPlan  # noqa: E402
+from das_diff_veh_amd.disp import DispPlan, fv_from_fk  # noqa: E402
 from das_diff_veh_amd.synth import synth_gathers  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip parameters
@@ -70,9 +70,7 @@ def main():
                   _lib.ptr(FK), None, None, st)
         if ev:
             ev[2].record(stream)
-        _lib.call("dvh_disp_fv", _lib.ptr(FK), B, plan.n_kb, plan.n_fb, _lib.ptr(tb["kgrid"]), plan.kmin, plan.kmax,
-                  _lib.ptr(tb["kq"]), plan.nF, plan.nV, _lib.ptr(tb["fj"]), _lib.ptr(tb["fw"]), _lib.ptr(tb["sg"]),
-                  plan.sgl, _lib.ptr(fv), st)
+        fv_from_fk(FK, plan, out=fv)  # the product dispatch (cell-staged tiles for a batch this size)
         if ev:
             ev[3].record(stream)
 
