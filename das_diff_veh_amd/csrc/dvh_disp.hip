@@ -650,6 +650,271 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
   }
 }
 
+// 3d. f-v sampling with the Savitzky-Golay filter on the matrix pipe.  The filter is a banded Toeplitz
+// operator along frequency, so a (16 velocities x 16 frequencies) output tile is one float64 MFMA GEMM
+//   out[v][f0 + j] = sum_{k < 40} x[v][f0 - 12 + k] * H[k][j],   H[k][j] = sg[k - j] (0 <= k - j < 25)
+// with the samples x as the A operand (A[i = v][k] on lane (v, k & 3)) and the band as B: 10 K-steps of
+// v_mfma_f64_16x16x4_f64 per tile (40 / 25 of the filter's FMAs, on the MFMA pipe, beside the VALU that
+// samples).  A wave owns 16 velocities of one image and walks the frequency axis tile by tile; tile t + 1
+// shares 24 of its 40 inputs with tile t, so each lane keeps its samples in a register ring (step g =
+// frequency 4 g - 12 + (lane >> 4), slot g & 15) and samples 4 new ones per tile, one tile ahead of the
+// MFMAs that consume them.  The first tile (left polynomial fit rows f < 12) and a last tile at
+// f0 = nF - 16 (right fit) take their B operands from the operator in LDS; the regular tiles write rows
+// f < nF - 16 only.  The block (4 waves, 64 velocities) stages each image's compact FK grid in LDS with
+// LDS-DMA (global_load_lds_dword, no VGPRs), the next image's while the current one is filtered.
+// Sampling per (f, v) is fv_kernel's arithmetic with the image-independent parts from plan tables
+// (DispPlan.mfma_tables): the FITPACK weights hx[f][v] = {fx (khi - q), fx (q - klo)} of the clamped
+// query and the cell offset cb[f][v] = m * n_fb + fj[f], bit-identical to what the other kernels compute.
+#ifndef DVH_FV_MF_WPE
+#define DVH_FV_MF_WPE 3  // waves per SIMD the MFMA f-v kernel is register-budgeted for (149 VGPRs unconstrained; LDS allows 5 blocks / CU)
+#endif
+#ifndef DVH_FV_MF_SB
+#define DVH_FV_MF_SB 1  // 1: one scheduling region per tile in the MFMA f-v kernel (0: the compiler's schedule)
+#endif
+#ifndef DVH_FV_MF_IL
+#define DVH_FV_MF_IL 0  // > 0: interleave each MFMA with this many VALU instructions (sched_group_barrier)
+#endif
+#ifndef DVH_FV_MF_BLDS
+#define DVH_FV_MF_BLDS 1  // 1: the interior band operands read from LDS per MFMA (20 VGPRs fewer)
+#endif
+#ifndef DVH_FV_MF_EXP
+#define DVH_FV_MF_EXP 0  // timing experiments only (wrong results): 1 no stores, 2 no sampling, 3 no MFMA
+#endif
+#ifndef DVH_FV_MF_NT
+#define DVH_FV_MF_NT 0  // 1: non-temporal f-v stores (measured 936 vs 704 us on the time-lapse batch: off)
+#endif
+constexpr int kMfV = 16;      // velocities per wave
+constexpr int kMfWaves = 4;   // waves per block
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+__device__ __forceinline__ double sg_coef(const double* sgs, int nF, int f, int xi) {
+  constexpr int L = 2 * kSgPad + 1, half = kSgPad;
+  int t;
+  const double* c;
+  if (f < half) {  // left fit: x[0, L)
+    t = xi;
+    c = sgs + L + f * L;
+  } else if (f >= nF - half) {  // right fit: x[nF - L, nF)
+    t = xi - (nF - L);
+    c = sgs + L + half * L + (f - (nF - half)) * L;
+  } else {
+    t = xi - f + half;
+    c = sgs;
+  }
+  return (t >= 0 && t < L) ? c[t] : 0.0;
+}
+
+__global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(DVH_FV_MF_WPE, DVH_FV_MF_WPE))) void fv_mfma_kernel(
+    const double* __restrict__ FK, int32_t B, int32_t G, int32_t n_kb, int32_t n_fb,
+    const double2* __restrict__ hx, const int32_t* __restrict__ cb, int32_t nF, int32_t nV,
+    const double2* __restrict__ fw, const double* __restrict__ sg, float* __restrict__ fv, int32_t n_vb, int32_t xcd_map) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int L = 2 * kSgPad + 1;
+  const int nfk = n_kb * n_fb;
+  const int nbuf = ((nfk + 31) & ~31);  // doubles of the FK buffer: whole 256-byte LDS-DMA pieces
+  double* fks = smem;                   // [nbuf]
+  double* sgs = smem + nbuf;            // taps + edge fits (L * L)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // block -> (velocity block, image group); XCD-aware when the velocity blocks split evenly over the 8
+  // XCDs (blocks are dealt round robin): every block of a velocity block then runs on one XCD and its
+  // (f, v) table slice stays in that XCD's L2
+  int vb, ig;
+  {
+    const int L0 = blockIdx.x;
+    if (xcd_map) {
+      const int per = n_vb >> 3, x = L0 & 7, k = L0 >> 3;
+      vb = x + 8 * (k % per);
+      ig = k / per;
+    } else {
+      vb = L0 % n_vb;
+      ig = L0 / n_vb;
+    }
+  }
+  const int b0 = ig * G, n_img = min(G, B - b0);
+  const int vw = vb * (kMfWaves * kMfV) + wave * kMfV;  // the wave's first velocity
+  const int li = lane & 15, kk = lane >> 4;
+
+  // LDS-DMA of image `img`'s FK grid into buffer `buf` (256-byte pieces dealt over the waves; lanes past
+  // the grid re-read its last dword, landing in the buffer's pad)
+  const int n_piece = (2 * nfk + 63) >> 6;
+  auto stage = [&](int img) {
+    const float* src = reinterpret_cast<const float*>(FK + (int64_t)img * nfk);
+    for (int p = wave; p < n_piece; p += kMfWaves) {
+      const int e = min(p * 64 + lane, 2 * nfk - 1);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + e), (lds_void*)(fks + p * 32), 4, 0, 0);
+    }
+  };
+  for (int e = tid; e < L * L; e += kMfWaves * 64) sgs[e] = sg[e];
+
+  // interior band: B[k][j] for K-step s = sg[4 s + k - j], in registers or (DVH_FV_MF_BLDS) read from a
+  // zero-padded LDS copy of the taps at every use
+#if DVH_FV_MF_BLDS
+  double* bpad = sgs + L * L;  // [64]: taps at 16 .. 40, zeros around
+  for (int e = tid; e < 64; e += kMfWaves * 64) bpad[e] = (e >= 16 && e < 16 + L) ? sg[e - 16] : 0.0;
+  const int boff = 16 + kk - li;  // in [1, 19]; + 4 s stays within [1, 55]
+#define BINT(s) bpad[boff + 4 * (s)]
+#else
+  double bint[10];
+#pragma unroll
+  for (int s = 0; s < 10; ++s) {
+    const int t = 4 * s + kk - li;
+    bint[s] = (t >= 0 && t < L) ? sgs[t] : 0.0;
+  }
+#define BINT(s) bint[s]
+#endif
+  const int t_reg = (nF - kMfV + kMfV - 1) / kMfV;  // regular tiles: rows [16 t, min(16 t + 16, nF - 16))
+
+  for (int it = 0; it < n_img; ++it) {
+    const int b = b0 + it;
+    const double* F = fks;
+    // one FK buffer (several blocks per CU keep the MFMA pipe busy while a block stages): the previous
+    // image's reads are done (first barrier), the DMA has landed (vmcnt, second barrier)
+    __syncthreads();
+    stage(b);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // the lane indices and sizes are laundered per image: the first and last tiles' samples, band values
+    // and store addresses do not depend on the image, and hoisting them out of the image loop would hold
+    // ~200 registers; recomputing them is a few VALU per tile
+    int li_, kk_, nF_, nV_, va_, vc_, fl_;
+    bool vok_;
+    auto launder = [&]() {  // also before the last tile: no common subexpression with tile 0 lives across the loop
+      li_ = li;
+      kk_ = kk;
+      nF_ = nF;
+      nV_ = nV;
+      asm volatile("" : "+v"(li_), "+v"(kk_), "+s"(nF_), "+s"(nV_));
+      va_ = vw + li_;
+      vok_ = va_ < nV_;
+      vc_ = min(va_, nV_ - 1);
+      fl_ = nF_ - kMfV;  // the last tile's first row
+    };
+    launder();
+    // one sample of this lane, branch-free (indices clamped, the value zeroed outside the grid):
+    // x[va_][f] rounded to float32 as map_fv's interp2d output.  Split in two stages for the regular
+    // tiles: the table loads (tload) one tile before the LDS corners and the arithmetic (tfinish).
+    struct Pend {
+      double2 w;
+      int base, fc;
+      bool in;
+    };
+    auto tload = [&](int f) -> Pend {
+      Pend p;
+#if DVH_FV_MF_EXP == 2
+      p.fc = f; p.in = true; p.base = 0; p.w = {0.0, 0.0};
+      return p;
+#endif
+      p.in = vok_ && f >= 0 && f < nF_;
+      p.fc = min(max(f, 0), nF_ - 1);
+      const int qi = p.fc * nV_ + vc_;
+      p.w = hx[qi];
+      p.base = cb[qi];
+      return p;
+    };
+    auto tfinish = [&](const Pend& p) -> double {
+#if DVH_FV_MF_EXP == 2
+      return (double)p.fc;
+#endif
+      const double2 y = fw[p.fc];  // per frequency: 16 lanes share it, an L1 hit
+      const double z00 = F[p.base], z01 = F[p.base + 1], z10 = F[p.base + n_fb], z11 = F[p.base + n_fb + 1];
+      const double val = (double)(float)(z00 * p.w.x * y.x + z01 * p.w.x * y.y + z10 * p.w.y * y.x +
+                                         z11 * p.w.y * y.y);
+      return p.in ? val : 0.0;
+    };
+    auto sample = [&](int f) -> double { return tfinish(tload(f)); };
+    float* out_b = fv + (int64_t)b * nV_ * nF_;
+    auto store = [&](doublex4 acc, int f0, int f_end) {
+      const int f = f0 + li_;
+      if (f >= f_end) return;
+#if DVH_FV_MF_EXP == 1
+      if (acc[0] != 1.2345e300) return;
+#endif
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int v = vw + kk_ + 4 * r;
+#if DVH_FV_MF_NT
+        if (v < nV_) __builtin_nontemporal_store((float)acc[r], out_b + (int64_t)v * nF_ + f);
+#else
+        if (v < nV_) out_b[(int64_t)v * nF_ + f] = (float)acc[r];
+#endif
+      }
+    };
+    // ring of samples: step g (frequency 4 g - 12 + kk) in slot g & 15; steps 4 t + 10 .. 4 t + 13 (tile
+    // t + 1's new ones) are finished during tile t from table loads issued during tile t - 1
+    double x[16];
+    x[0] = x[1] = 0.0;  // frequencies < -4
+#pragma unroll
+    for (int s = 2; s < 14; ++s) {  // in groups of 4 loads in flight: the next group's addresses wait on
+      x[s] = sample(4 * s - 12 + kk_);  // this group's samples (an opaque dependency the compiler keeps)
+      if (s % 4 == 1) asm volatile("" : "+v"(kk_) : "v"(x[s - 3]), "v"(x[s - 2]), "v"(x[s - 1]), "v"(x[s]));
+    }
+    Pend pd[4];  // table loads of steps 14 .. 17 (tile 2's new ones), in flight during tile 0 and tile 1
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pd[i] = tload(4 * (14 + i) - 12 + kk_);
+    {  // tile 0: left-fit rows, B operands from the fit matrices in LDS
+      doublex4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 10; ++s) acc = mfma_f64(x[s], sg_coef(sgs, nF_, li_, 4 * s - 12 + kk_), acc);
+      store(acc, 0, min(kMfV, fl_));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // regular tiles t = 1 .. t_reg - 1, four per iteration so that the ring slots are static.  Tile t
+    // consumes steps 4 t .. 4 t + 9; during it, steps 4 t + 10 .. 4 t + 13 are finished from pd (loaded
+    // during tile t - 1) and steps 4 t + 14 .. 4 t + 17 are loaded into pd.
+    for (int t0 = 1; t0 < t_reg; t0 += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u;
+        if (t >= t_reg) break;
+        Pend nx[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nx[i] = tload(16 * t + 44 + 4 * i + kk_);
+        // steps 4 t + 10 + i -> slot (4 (u + 1) + 10 + i) & 15  (t = t0 + u, t0 = 1 mod 4)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[(4 * (u + 1) + 10 + i) & 15] = tfinish(pd[i]);
+        doublex4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+#if DVH_FV_MF_EXP == 3
+        for (int s = 0; s < 10; ++s) acc[s & 3] += x[(4 * (u + 1) + s) & 15];
+#else
+        for (int s = 0; s < 10; ++s) acc = mfma_f64(x[(4 * (u + 1) + s) & 15], BINT(s), acc);
+#endif
+        store(acc, kMfV * t, fl_);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pd[i] = nx[i];
+#if DVH_FV_MF_SB
+        // one tile per scheduling region; the MFMAs interleaved with the finishing arithmetic
+        asm volatile("" ::"v"(x[(4 * (u + 1) + 10) & 15]), "v"(x[(4 * (u + 1) + 11) & 15]),
+                     "v"(x[(4 * (u + 1) + 12) & 15]), "v"(x[(4 * (u + 1) + 13) & 15]));
+#if DVH_FV_MF_IL
+#pragma unroll
+        for (int s = 0; s < 10; ++s) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, DVH_FV_MF_IL, 0);  // then VALU
+        }
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+      }
+    }
+    launder();
+    {  // last tile: rows nF - 16 .. nF - 1 (right fit), fresh samples in two groups of 5
+      doublex4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 10; ++s) {
+        const int xi = fl_ - 12 + 4 * s + kk_;
+        const double xs = sample(xi);
+        acc = mfma_f64(xs, sg_coef(sgs, nF_, fl_ + li_, xi), acc);
+        if (s == 4) asm volatile("" : "+v"(kk_) : "v"(xs));
+      }
+      store(acc, fl_, nF_);
+    }
+  }
+}
+
+#undef BINT
+
 // per-row L1 norms -> 1 / ||row||_1 (map_fv norm=True: data / norm(data, ord=1, axis=-1))
 __global__ __launch_bounds__(256) void row_l1_kernel(const float* __restrict__ data, int64_t b_stride,
                                                       int64_t ch_stride, int32_t nch, int32_t nt,
@@ -838,5 +1103,33 @@ DVH_API int dvh_disp_fv_cells(const double* FK, int32_t B, int32_t n_kb, int32_t
   hipLaunchKernelGGL((fv_tile_kernel<kFvVT, true>), grid, dim3(kTileThreads), lds, (hipStream_t)stream, FK, B, G, n_kb,
                      n_fb, kgrid, kmin, kmax, kq, nF, nV, TO, (const int32_t*)nullptr, fw, sg, sgl, fv, cell_off, n_cell,
                      max_cell, (const int4*)qidx);
+  return last_launch();
+}
+
+DVH_API int dvh_disp_fv_mfma(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, const double* hx,
+                             const int32_t* cb, int32_t nF, int32_t nV, const double* fw, const double* sg, int32_t sgl,
+                             int32_t G, float* fv, void* stream) {
+  if (!FK || !hx || !cb || !fw || !sg || !fv) return set_error(-2, "null pointer argument");
+  if (n_kb < 2 || n_fb < 2) return set_error(-2, "FK grid needs at least 2 x 2 bins");
+  if (sgl != 2 * kSgPad + 1) return set_error(-4, "the MFMA f-v kernel is built for savgol window 25");
+  if (nF < 2 * kMfV) return set_error(-4, "the MFMA f-v kernel needs at least 32 frequencies");
+  if ((int64_t)n_kb * n_fb > 8192) return set_error(-4, "FK grid larger than 8192 bins");
+  if ((int64_t)nF * nV > 0x7fffffff) return set_error(-4, "f-v grid larger than 2^31 points");
+  if (B <= 0 || nV <= 0) return 0;
+  const int nfk = n_kb * n_fb, nbuf = (nfk + 31) & ~31;
+  const size_t lds = sizeof(double) * ((size_t)nbuf + (size_t)sgl * sgl + 64);
+  hipError_t e = hipFuncSetAttribute((const void*)fv_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+  const int n_vb = (nV + kMfWaves * kMfV - 1) / (kMfWaves * kMfV);
+  if (G <= 0) {  // ~2 k blocks, at most 16 images each
+    G = (int)(((int64_t)n_vb * B) / 2048);
+    G = G < 1 ? 1 : (G > 16 ? 16 : G);
+  }
+  const int n_ig = (B + G - 1) / G;
+  const int xcd_map = (n_vb % 8 == 0) ? 1 : 0;
+  const int64_t n_blk = (int64_t)n_vb * n_ig;
+  if (n_blk > 0x7fffffff) return set_error(-4, "grid too large");
+  hipLaunchKernelGGL(fv_mfma_kernel, dim3((unsigned)n_blk), dim3(kMfWaves * 64), lds, (hipStream_t)stream, FK, B, G,
+                     n_kb, n_fb, (const double2*)hx, cb, nF, nV, (const double2*)fw, sg, fv, n_vb, xcd_map);
   return last_launch();
 }

@@ -179,6 +179,21 @@ class DispPlan:
         self._cells = dict(TO=TO, n_tile=nt, max_cell=max_cell, cell_off=cell_off, n_cell=ncell, qidx=qidx)
         return self._cells
 
+    def mfma_tables(self):
+        """dvh_disp_fv_mfma's per-(f, v) tables (cached): the FITPACK degree-1 weights of every clamped query
+        on its interval m, hx[f][v] = (fx * (khi - q), fx * (q - klo)) with fx = 1 / (khi - klo) -- the
+        expressions the sampling kernels evaluate, so the values are bit-identical -- and the compact cell
+        offset cb[f][v] = m * n_fb + fj[f]."""
+        if getattr(self, "_mfma", None) is None:
+            q = np.clip(self.kq, self.kmin, self.kmax)
+            m = self.mk.astype(np.int64)
+            klo, khi = self.kgrid[m], self.kgrid[m + 1]
+            fx = 1.0 / (khi - klo)
+            hx = np.stack([fx * (khi - q), fx * (q - klo)], axis=-1)
+            cb = (m * self.n_fb + self.fj.astype(np.int64)[:, None]).astype(np.int32)
+            self._mfma = dict(hx=np.ascontiguousarray(hx), cb=np.ascontiguousarray(cb))
+        return self._mfma
+
     def tables(self, device):
         key = str(device)
         if key not in self._dev:
@@ -236,12 +251,38 @@ def _use_cells(plan: DispPlan, B: int) -> bool:
     return plan.cell_tables() is not None
 
 
+def _use_mfma(plan: DispPlan, B: int) -> bool:
+    """The MFMA-filter kernel (dvh_disp_fv_mfma) where it applies: savgol window 25, nF >= 32, a compact FK
+    grid of at most 8 192 bins.  DVH_FV_MFMA=0 / 1 forces it off / on (A/B)."""
+    ok = plan.sgl == 25 and plan.nF >= 32 and plan.n_kb * plan.n_fb <= 8192
+    env = os.environ.get("DVH_FV_MFMA")
+    if env is not None:
+        return env != "0" and ok
+    if any(k in os.environ for k in ("DVH_FV_TILE", "DVH_FV_G", "DVH_FV_CELLS")):  # A/B of the other kernels
+        return False
+    return ok and B * -(-plan.nV // 64) >= MFMA_MIN_BLOCKS
+
+
+MFMA_MIN_BLOCKS = 512  # (64-velocity block, image) pairs: two blocks per CU
+
+
 def fv_from_fk(FK, plan: DispPlan, out=None):
     dev = FK.device
     tb = plan.tables(dev)
     B = FK.shape[0]
     if out is None:
         out = torch.empty((B, plan.nV, plan.nF), dtype=torch.float32, device=dev)
+    if _use_mfma(plan, B):
+        key = ("mfma", str(dev))
+        if key not in plan._dev:
+            mt = plan.mfma_tables()
+            plan._dev[key] = {k: torch.from_numpy(v).to(dev) for k, v in mt.items()}
+        mt = plan._dev[key]
+        G = int(os.environ.get("DVH_FV_MG", "0"))
+        _lib.call("dvh_disp_fv_mfma", _lib.ptr(FK), B, plan.n_kb, plan.n_fb, _lib.ptr(mt["hx"]), _lib.ptr(mt["cb"]),
+                  plan.nF, plan.nV, _lib.ptr(tb["fw"]), _lib.ptr(tb["sg"]), plan.sgl, G, _lib.ptr(out),
+                  _lib.stream_of(dev))
+        return out
     if _use_cells(plan, B):
         key = ("cells", str(dev))
         if key not in plan._dev:

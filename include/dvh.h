@@ -138,6 +138,17 @@ int dvh_disp_fv_cells(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, c
                       int32_t sgl, int32_t TO, int32_t n_tile, int32_t VT, int32_t max_cell, const int32_t* cell_off,
                       const int32_t* n_cell, const int32_t* qidx, float* fv, void* stream);
 
+/* dvh_disp_fv with the Savitzky-Golay filter on the float64 matrix pipe (map_fv's savgol,
+ * modules/utils.py:473): each (16 velocities x 16 frequencies) output tile is one banded GEMM of
+ * 10 v_mfma_f64_16x16x4_f64 steps over the float32-rounded bilinear samples.  Plan tables
+ * (DispPlan.mfma_tables): hx[nF][nV][2] float64 = the FITPACK weights {fx (khi - q), fx (q - klo)} of
+ * every clamped query on its interval m, cb[nF][nV] int32 = m * n_fb + fj[f] (the (m, j) cell of the
+ * compact grid), fw[nF][2] as dvh_disp_fv.  G images per block (0: chosen by the launcher).  Needs
+ * sgl == 25, nF >= 32, n_kb * n_fb <= 8192.  Same outputs as dvh_disp_fv. */
+int dvh_disp_fv_mfma(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, const double* hx, const int32_t* cb,
+                     int32_t nF, int32_t nV, const double* fw, const double* sg, int32_t sgl, int32_t G, float* fv,
+                     void* stream);
+
 /* ---------------------------------------------------------------- bootstrap / convergence
  * bootstrap_disp (apis/imaging_classes.py:8-48): per-pass gathers once, then per resample the mean
  * stack, its f-v image (dvh_disp_*) and the ridge picks (extract_ridge_ref_idx, modules/utils.py:621-678). */

@@ -11,12 +11,13 @@ TOL = 1e-4
 
 @pytest.mark.parametrize("mode", [None, ("DVH_FV_TILE", "2"), ("DVH_FV_TILE", "0"), ("DVH_FV_G", "3"),
                                   ("DVH_FV_G", "16"), ("DVH_FV_TG", "3"), ("DVH_FV_G", "0"), ("DVH_FV_CELLS", "1"),
-                                  ("DVH_FV_CELLS", "0")])
+                                  ("DVH_FV_CELLS", "0"), ("DVH_FV_MFMA", "1"), ("DVH_FV_MG", "3")])
 @pytest.mark.parametrize("B,nv,nf", [(40, 512, 1000), (7, 300, 242), (5, 64, 1001), (3, 61, 25), (4, 33, 413)])
 def test_fv_batch_vs_oracle(device, monkeypatch, B, nv, nf, mode):
     """mode: kernel selection read at each launch -- None = default dispatch, DVH_FV_TILE=2 -> always
     the frequency-tiled kernel, DVH_FV_TILE=0 -> batched / per-image dispatch, DVH_FV_G = images per block of the batched kernel (0: per-image
-    kernel), DVH_FV_TG = images per block of the tiled kernel."""
+    kernel), DVH_FV_TG = images per block of the tiled kernel, DVH_FV_MFMA=1 -> the MFMA-filter kernel where
+    it applies (nF >= 32), DVH_FV_MG = its images per block."""
     if mode is not None:
         if mode[0] == "DVH_FV_G":
             monkeypatch.setenv("DVH_FV_TILE", "0")
@@ -24,6 +25,8 @@ def test_fv_batch_vs_oracle(device, monkeypatch, B, nv, nf, mode):
             monkeypatch.setenv("DVH_FV_TILE", "2")
         if mode == ("DVH_FV_CELLS", "1"):  # also split the images over several blocks
             monkeypatch.setenv("DVH_FV_TG", "3")
+        if mode[0] == "DVH_FV_MG":  # MFMA-filter kernel, 3 images per block
+            monkeypatch.setenv("DVH_FV_MFMA", "1")
         monkeypatch.setenv(*mode)
     from das_diff_veh_amd.disp import DispPlan, fv_maps
     from das_diff_veh_amd.synth import synth_gathers

@@ -379,3 +379,34 @@ def test_fv_cell_tables_address_every_stencil_cell(nv, nf):
     # the point of the tables: a block stages a few rows per column, not the n_kb rows
     assert ct["max_cell"] < 0.5 * plan.n_kb * plan.n_fb
     print("cells per block", int(ct["n_cell"].mean()), "of", plan.n_kb * plan.n_fb)
+
+
+@pytest.mark.parametrize("nv,nf", [(1000, 242), (512, 1000), (61, 33)])
+def test_fv_mfma_tables_reproduce_interp2d(nv, nf):
+    """DispPlan.mfma_tables (dvh_disp_fv_mfma): the per-(f, v) FITPACK weights hx and compact cell offsets
+    cb, combined the way the kernel does (z00 hx0 hy0 + z01 hx0 hy1 + z10 hx1 hy0 + z11 hx1 hy1), give the
+    oracle's interp2d bilinear samples (oracle/disp.py bilinear, modules/utils.py:466-472) on a random
+    full FK grid to float64 rounding, and the weights are those of the plan's own intervals."""
+    from das_diff_veh_amd.disp import DispPlan
+    from oracle import disp as odisp
+    dt = 0.003999999999997783
+    freqs = np.arange(0.8, 25, 0.1) if nf == 242 else np.linspace(1.0, 24.0, nf)
+    vels = np.arange(200, 200 + nv) if nv == 1000 else np.linspace(150.0, 1200.0, nv)
+    plan = DispPlan(25, 500, 8.16, dt, freqs, vels)
+    mt = plan.mfma_tables()
+    hx, cb = mt["hx"], mt["cb"]
+    assert hx.shape == (plan.nF, plan.nV, 2) and hx.dtype == np.float64
+    assert cb.shape == (plan.nF, plan.nV) and cb.dtype == np.int32
+    rng = np.random.default_rng(1)
+    res = rng.random((plan.nk, plan.nf))
+    comp = res[plan.m_lo:plan.m_lo + plan.n_kb, plan.j_lo:plan.j_lo + plan.n_fb].ravel()
+    for f in range(0, plan.nF, max(1, plan.nF // 17)):
+        base = cb[f]
+        hy0, hy1 = plan.fw[f]
+        got = (comp[base] * hx[f, :, 0] * hy0 + comp[base + 1] * hx[f, :, 0] * hy1
+               + comp[base + plan.n_fb] * hx[f, :, 1] * hy0 + comp[base + plan.n_fb + 1] * hx[f, :, 1] * hy1)
+        ref = odisp.bilinear(res, plan.fft_f, plan.fft_k, np.divide(np.ones(plan.nV) * plan.freqs[f], plan.vels),
+                             plan.freqs[f])
+        assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max(), f
+    assert np.array_equal(cb // plan.n_fb, plan.mk)
+    assert np.all(cb % plan.n_fb == plan.fj[:, None])

@@ -6,7 +6,8 @@ One step = the f-v images of B gathers (one day's stacks at B pivots, the [-200,
 -> Dispersion -> map_fv, modules/utils.py:383-426, 457-475), through the dispersion kernels:
   tdft_gemm_kernel    time DFT as a real float64 MFMA GEMM [B*nch x nt] . [nt x 2*n_fb]
   fk_contract_kernel  channel contraction, complex float64 MFMA GEMM per gather, |.|
-  fv_kernel           FITPACK bilinear sampling + Savitzky-Golay(25, 4), float32 out
+  fv_*_kernel         FITPACK bilinear sampling + Savitzky-Golay(25, 4), float32 out (the product dispatch:
+                      fv_mfma_kernel, the filter as banded float64 MFMA GEMMs, for a batch this size)
 Per-kernel durations come from HIP events on the launch stream; the GEMM rooflines are priced
 against the float64 MFMA peak, fv_kernel against HBM (it writes 4 * nV * nF bytes per image).
 The gathers are synthetic (dispersive tones c(f) = 250 + 4000 / (f + 4), noise), resident on the
@@ -98,6 +99,11 @@ def main():
     tdft_flop = 2.0 * M * K * N
     fk_flop = 2.0 * B * (2 * plan.MT) * plan.K2 * plan.n_fb
     fv_bytes = 4.0 * B * plan.nV * plan.nF + 8.0 * B * plan.n_kb * plan.n_fb
+    from das_diff_veh_amd.disp import _use_mfma
+    mfma = _use_mfma(plan, B)
+    fir_flop = 2.0 * 25 * B * plan.nV * plan.nF
+    n_tiles = -(-(plan.nF - 16) // 16) + 1
+    mfma_flop = 2.0 * 16 * 16 * 40 * n_tiles * B * -(-plan.nV // 16)
     res = {
         "metric": "time-lapse f-v images/s (configs[4]: 512 velocities x 1,000 frequencies, batched MFMA dispersion)",
         "value": B / step, "unit": "f-v images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -111,7 +117,12 @@ def main():
             "fk_contract_kernel": {"us": t[1] * 1e6, "flop": fk_flop, "achieved_tflops": fk_flop / t[1] / 1e12,
                                    "peak_tflops": FP64_MFMA_PEAK_TF, "frac": fk_flop / t[1] / 1e12 / FP64_MFMA_PEAK_TF},
             "fv_kernel": {"us": t[2] * 1e6, "bytes": fv_bytes, "achieved_gbs": fv_bytes / t[2] / 1e9,
-                          "peak_gbs": HBM_PEAK_GBS, "frac": fv_bytes / t[2] / 1e9 / HBM_PEAK_GBS},
+                          "peak_gbs": HBM_PEAK_GBS, "frac": fv_bytes / t[2] / 1e9 / HBM_PEAK_GBS,
+                          "kernel": "fv_mfma_kernel" if mfma else "fv_tile_kernel / fv_batch_kernel / fv_kernel",
+                          # the Savitzky-Golay FIR (25 taps per output) and, for the MFMA kernel, the FLOPs it issues
+                          # (10 v_mfma_f64_16x16x4_f64 per 16 x 16 tile, ceil((nF - 16) / 16) + 1 tiles per row)
+                          "fir_flop": fir_flop, "mfma_flop_issued": mfma_flop if mfma else 0.0,
+                          "mfma_frac": (mfma_flop / t[2] / 1e12 / FP64_MFMA_PEAK_TF) if mfma else None},
         },
         "parity": {"max_rel_err": max(errs), "picks_ok": all(picks), "images_checked": 2, "tol": 1e-4},
     }
