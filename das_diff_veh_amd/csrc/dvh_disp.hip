@@ -655,33 +655,34 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 //   out[v][f0 + j] = sum_{k < 40} x[v][f0 - 12 + k] * H[k][j],   H[k][j] = sg[k - j] (0 <= k - j < 25)
 // with the samples x as the A operand (A[i = v][k] on lane (v, k & 3)) and the band as B: 10 K-steps of
 // v_mfma_f64_16x16x4_f64 per tile (40 / 25 of the filter's FMAs, on the MFMA pipe, beside the VALU that
-// samples).  A wave owns 16 velocities of one image and walks the frequency axis tile by tile; tile t + 1
-// shares 24 of its 40 inputs with tile t, so each lane keeps its samples in a register ring (step g =
-// frequency 4 g - 12 + (lane >> 4), slot g & 15) and samples 4 new ones per tile, one tile ahead of the
-// MFMAs that consume them.  The first tile (left polynomial fit rows f < 12) and a last tile at
+// samples).  A wave owns 16 velocities of GI images (GI independent accumulation chains) and walks the
+// frequency axis tile by tile; tile t + 1 shares 24 of its 40 inputs with tile t, so each lane keeps its
+// samples in a register ring per image (step g = frequency 4 g - 12 + (lane >> 4), slot g & 15) and
+// samples 4 new ones per tile: their table loads one tile ahead, their arithmetic during the tile before
+// the MFMAs that consume them.  The first tile (left polynomial fit rows f < 12) and a last tile at
 // f0 = nF - 16 (right fit) take their B operands from the operator in LDS; the regular tiles write rows
-// f < nF - 16 only.  The block (4 waves, 64 velocities) stages each image's compact FK grid in LDS with
-// LDS-DMA (global_load_lds_dword, no VGPRs), the next image's while the current one is filtered.
+// f < nF - 16 only.  The block (4 waves, 64 velocities) stages the GI images' compact FK grids in LDS
+// with LDS-DMA (global_load_lds_dword, no VGPRs).
 // Sampling per (f, v) is fv_kernel's arithmetic with the image-independent parts from plan tables
-// (DispPlan.mfma_tables): the FITPACK weights hx[f][v] = {fx (khi - q), fx (q - klo)} of the clamped
-// query and the cell offset cb[f][v] = m * n_fb + fj[f], bit-identical to what the other kernels compute.
+// (DispPlan.mfma_tables), loaded once per sample for the GI images: the FITPACK weights hx[f][v] =
+// {fx (khi - q), fx (q - klo)} of the clamped query and the cell offset cb[f][v] = m * n_fb + fj[f],
+// bit-identical to what the other kernels compute.  (Forming the weights in the kernel from the query and
+// LDS tables of the k grid and fw measured slower: 1 207 vs 704 us for one image per wave, the LDS
+// bandwidth of the extra reads.)  Two images per wave (GI = 2) measured 673 vs 724 us for one.
+#ifndef DVH_FV_MF_GI
+#define DVH_FV_MF_GI 2  // images per wave in lock step (1 or 2)
+#endif
 #ifndef DVH_FV_MF_WPE
-#define DVH_FV_MF_WPE 3  // waves per SIMD the MFMA f-v kernel is register-budgeted for (149 VGPRs unconstrained; LDS allows 5 blocks / CU)
+#define DVH_FV_MF_WPE (DVH_FV_MF_GI == 1 ? 3 : 2)  // waves per SIMD the kernel is register-budgeted for
 #endif
 #ifndef DVH_FV_MF_SB
 #define DVH_FV_MF_SB 1  // 1: one scheduling region per tile in the MFMA f-v kernel (0: the compiler's schedule)
 #endif
-#ifndef DVH_FV_MF_IL
-#define DVH_FV_MF_IL 0  // > 0: interleave each MFMA with this many VALU instructions (sched_group_barrier)
-#endif
-#ifndef DVH_FV_MF_BLDS
-#define DVH_FV_MF_BLDS 1  // 1: the interior band operands read from LDS per MFMA (20 VGPRs fewer)
+#ifndef DVH_FV_MF_PAIR
+#define DVH_FV_MF_PAIR 0  // 1: finish the 4 new samples of a tile two at a time (fewer registers; 700 vs 684 us)
 #endif
 #ifndef DVH_FV_MF_EXP
 #define DVH_FV_MF_EXP 0  // timing experiments only (wrong results): 1 no stores, 2 no sampling, 3 no MFMA
-#endif
-#ifndef DVH_FV_MF_NT
-#define DVH_FV_MF_NT 0  // 1: non-temporal f-v stores (measured 936 vs 704 us on the time-lapse batch: off)
 #endif
 constexpr int kMfV = 16;      // velocities per wave
 constexpr int kMfWaves = 4;   // waves per block
@@ -705,16 +706,25 @@ __device__ __forceinline__ double sg_coef(const double* sgs, int nF, int f, int 
   return (t >= 0 && t < L) ? c[t] : 0.0;
 }
 
+// LDS bytes of fv_mfma_kernel<GI>
+__host__ __device__ inline size_t fv_mfma_lds(int GI, int nfk) {
+  const int nbuf = (nfk + 31) & ~31;
+  constexpr int L = 2 * kSgPad + 1;
+  return sizeof(double) * ((size_t)GI * nbuf + (size_t)L * L + 64);
+}
+
+template <int GI>
 __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(DVH_FV_MF_WPE, DVH_FV_MF_WPE))) void fv_mfma_kernel(
-    const double* __restrict__ FK, int32_t B, int32_t G, int32_t n_kb, int32_t n_fb,
-    const double2* __restrict__ hx, const int32_t* __restrict__ cb, int32_t nF, int32_t nV,
-    const double2* __restrict__ fw, const double* __restrict__ sg, float* __restrict__ fv, int32_t n_vb, int32_t xcd_map) {
+    const double* __restrict__ FK, int32_t B, int32_t G, int32_t n_kb, int32_t n_fb, const double2* __restrict__ hx,
+    const int32_t* __restrict__ cb, int32_t nF, int32_t nV, const double2* __restrict__ fw, const double* __restrict__ sg,
+    float* __restrict__ fv, int32_t n_vb, int32_t xcd_map) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int L = 2 * kSgPad + 1;
   const int nfk = n_kb * n_fb;
-  const int nbuf = ((nfk + 31) & ~31);  // doubles of the FK buffer: whole 256-byte LDS-DMA pieces
-  double* fks = smem;                   // [nbuf]
-  double* sgs = smem + nbuf;            // taps + edge fits (L * L)
+  const int nbuf = ((nfk + 31) & ~31);  // doubles of an FK buffer: whole 256-byte LDS-DMA pieces
+  double* fks = smem;                   // [GI][nbuf]
+  double* sgs = smem + GI * nbuf;       // taps + edge fits (L * L)
+  double* bpad = sgs + L * L;           // [64]: taps at 16 .. 40, zeros around (the interior band)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // block -> (velocity block, image group); XCD-aware when the velocity blocks split evenly over the 8
   // XCDs (blocks are dealt round robin): every block of a velocity block then runs on one XCD and its
@@ -738,44 +748,28 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
   // LDS-DMA of image `img`'s FK grid into buffer `buf` (256-byte pieces dealt over the waves; lanes past
   // the grid re-read its last dword, landing in the buffer's pad)
   const int n_piece = (2 * nfk + 63) >> 6;
-  auto stage = [&](int img) {
+  auto stage = [&](int img, int buf) {
     const float* src = reinterpret_cast<const float*>(FK + (int64_t)img * nfk);
     for (int p = wave; p < n_piece; p += kMfWaves) {
       const int e = min(p * 64 + lane, 2 * nfk - 1);
-      __builtin_amdgcn_global_load_lds((gbl_void*)(src + e), (lds_void*)(fks + p * 32), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(src + e), (lds_void*)(fks + buf * nbuf + p * 32), 4, 0, 0);
     }
   };
   for (int e = tid; e < L * L; e += kMfWaves * 64) sgs[e] = sg[e];
-
-  // interior band: B[k][j] for K-step s = sg[4 s + k - j], in registers or (DVH_FV_MF_BLDS) read from a
-  // zero-padded LDS copy of the taps at every use
-#if DVH_FV_MF_BLDS
-  double* bpad = sgs + L * L;  // [64]: taps at 16 .. 40, zeros around
   for (int e = tid; e < 64; e += kMfWaves * 64) bpad[e] = (e >= 16 && e < 16 + L) ? sg[e - 16] : 0.0;
-  const int boff = 16 + kk - li;  // in [1, 19]; + 4 s stays within [1, 55]
-#define BINT(s) bpad[boff + 4 * (s)]
-#else
-  double bint[10];
-#pragma unroll
-  for (int s = 0; s < 10; ++s) {
-    const int t = 4 * s + kk - li;
-    bint[s] = (t >= 0 && t < L) ? sgs[t] : 0.0;
-  }
-#define BINT(s) bint[s]
-#endif
+  const int boff = 16 + kk - li;  // interior band B[k][j] of K-step s = bpad[boff + 4 s] = sg[4 s + k - j]
   const int t_reg = (nF - kMfV + kMfV - 1) / kMfV;  // regular tiles: rows [16 t, min(16 t + 16, nF - 16))
 
-  for (int it = 0; it < n_img; ++it) {
-    const int b = b0 + it;
-    const double* F = fks;
-    // one FK buffer (several blocks per CU keep the MFMA pipe busy while a block stages): the previous
-    // image's reads are done (first barrier), the DMA has landed (vmcnt, second barrier)
+  for (int it = 0; it < n_img; it += GI) {
+    const int ng = min(GI, n_img - it);  // images of this pass (a lone last image runs as a pair with itself)
+    // the previous pass's reads are done (first barrier), the DMA has landed (vmcnt, second barrier)
     __syncthreads();
-    stage(b);
+#pragma unroll
+    for (int g = 0; g < GI; ++g) stage(b0 + it + min(g, ng - 1), g);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // the lane indices and sizes are laundered per image: the first and last tiles' samples, band values
-    // and store addresses do not depend on the image, and hoisting them out of the image loop would hold
+    // the lane indices and sizes are laundered per pass: the first and last tiles' samples, band values
+    // and store addresses do not depend on the images, and hoisting them out of the image loop would hold
     // ~200 registers; recomputing them is a few VALU per tile
     int li_, kk_, nF_, nV_, va_, vc_, fl_;
     bool vok_;
@@ -791,9 +785,9 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
       fl_ = nF_ - kMfV;  // the last tile's first row
     };
     launder();
-    // one sample of this lane, branch-free (indices clamped, the value zeroed outside the grid):
-    // x[va_][f] rounded to float32 as map_fv's interp2d output.  Split in two stages for the regular
-    // tiles: the table loads (tload) one tile before the LDS corners and the arithmetic (tfinish).
+    // one sample of this lane for the GI images, branch-free (indices clamped, values zeroed outside the
+    // grid): x[va_][f] rounded to float32 as map_fv's interp2d output.  Two stages for the regular
+    // tiles: the table loads (tload) one tile before the weights, corners and arithmetic (tfinish).
     struct Pend {
       double2 w;
       int base, fc;
@@ -801,61 +795,76 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
     };
     auto tload = [&](int f) -> Pend {
       Pend p;
-#if DVH_FV_MF_EXP == 2
-      p.fc = f; p.in = true; p.base = 0; p.w = {0.0, 0.0};
-      return p;
-#endif
       p.in = vok_ && f >= 0 && f < nF_;
       p.fc = min(max(f, 0), nF_ - 1);
+#if DVH_FV_MF_EXP == 2
+      p.w = {0.0, 0.0}; p.base = 0;
+      return p;
+#endif
       const int qi = p.fc * nV_ + vc_;
       p.w = hx[qi];
       p.base = cb[qi];
       return p;
     };
-    auto tfinish = [&](const Pend& p) -> double {
+    auto tfinish = [&](const Pend& p, double* xo) {
 #if DVH_FV_MF_EXP == 2
-      return (double)p.fc;
-#endif
-      const double2 y = fw[p.fc];  // per frequency: 16 lanes share it, an L1 hit
-      const double z00 = F[p.base], z01 = F[p.base + 1], z10 = F[p.base + n_fb], z11 = F[p.base + n_fb + 1];
-      const double val = (double)(float)(z00 * p.w.x * y.x + z01 * p.w.x * y.y + z10 * p.w.y * y.x +
-                                         z11 * p.w.y * y.y);
-      return p.in ? val : 0.0;
-    };
-    auto sample = [&](int f) -> double { return tfinish(tload(f)); };
-    float* out_b = fv + (int64_t)b * nV_ * nF_;
-    auto store = [&](doublex4 acc, int f0, int f_end) {
-      const int f = f0 + li_;
-      if (f >= f_end) return;
-#if DVH_FV_MF_EXP == 1
-      if (acc[0] != 1.2345e300) return;
-#endif
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int v = vw + kk_ + 4 * r;
-#if DVH_FV_MF_NT
-        if (v < nV_) __builtin_nontemporal_store((float)acc[r], out_b + (int64_t)v * nF_ + f);
-#else
-        if (v < nV_) out_b[(int64_t)v * nF_ + f] = (float)acc[r];
+      for (int g = 0; g < GI; ++g) xo[g] = (double)p.fc;
+      return;
 #endif
+      const double2 y = fw[p.fc];  // per frequency: 16 lanes share it (an LDS copy measured slower: the
+                                   // corner reads already load the LDS, 700 vs 673 us)
+      const int base = p.base;
+#pragma unroll
+      for (int g = 0; g < GI; ++g) {
+        const double* F = fks + g * nbuf;
+        const double z00 = F[base], z01 = F[base + 1], z10 = F[base + n_fb], z11 = F[base + n_fb + 1];
+        const double val = (double)(float)(z00 * p.w.x * y.x + z01 * p.w.x * y.y + z10 * p.w.y * y.x +
+                                           z11 * p.w.y * y.y);
+        xo[g] = p.in ? val : 0.0;
       }
     };
-    // ring of samples: step g (frequency 4 g - 12 + kk) in slot g & 15; steps 4 t + 10 .. 4 t + 13 (tile
+    auto sample = [&](int f, double* xo) { tfinish(tload(f), xo); };
+    auto store = [&](const doublex4* acc, int f0, int f_end) {
+      const int f = f0 + li_;
+      if (f >= f_end) return;
+#pragma unroll
+      for (int g = 0; g < GI; ++g) {
+        if (g >= ng) break;
+#if DVH_FV_MF_EXP == 1
+        if (acc[g][0] != 1.2345e300) return;
+#endif
+        float* out_b = fv + (int64_t)(b0 + it + g) * nV_ * nF_;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int v = vw + kk_ + 4 * r;
+          if (v < nV_) out_b[(int64_t)v * nF_ + f] = (float)acc[g][r];
+        }
+      }
+    };
+    // rings of samples: step g (frequency 4 g - 12 + kk) in slot g & 15; steps 4 t + 10 .. 4 t + 13 (tile
     // t + 1's new ones) are finished during tile t from table loads issued during tile t - 1
-    double x[16];
-    x[0] = x[1] = 0.0;  // frequencies < -4
+    double x[16][GI];
+#pragma unroll
+    for (int g = 0; g < GI; ++g) x[0][g] = x[1][g] = 0.0;  // frequencies < -4
 #pragma unroll
     for (int s = 2; s < 14; ++s) {  // in groups of 4 loads in flight: the next group's addresses wait on
-      x[s] = sample(4 * s - 12 + kk_);  // this group's samples (an opaque dependency the compiler keeps)
-      if (s % 4 == 1) asm volatile("" : "+v"(kk_) : "v"(x[s - 3]), "v"(x[s - 2]), "v"(x[s - 1]), "v"(x[s]));
+      sample(4 * s - 12 + kk_, x[s]);  // this group's samples (an opaque dependency the compiler keeps)
+      if (s % 4 == 1) asm volatile("" : "+v"(kk_) : "v"(x[s - 3][0]), "v"(x[s - 2][0]), "v"(x[s - 1][0]), "v"(x[s][0]));
     }
-    Pend pd[4];  // table loads of steps 14 .. 17 (tile 2's new ones), in flight during tile 0 and tile 1
+    Pend pd[4];  // table loads of steps 14 .. 17 (tile 2's new ones), in flight during tiles 0 and 1
 #pragma unroll
     for (int i = 0; i < 4; ++i) pd[i] = tload(4 * (14 + i) - 12 + kk_);
     {  // tile 0: left-fit rows, B operands from the fit matrices in LDS
-      doublex4 acc = {0.0, 0.0, 0.0, 0.0};
+      doublex4 acc[GI];
 #pragma unroll
-      for (int s = 0; s < 10; ++s) acc = mfma_f64(x[s], sg_coef(sgs, nF_, li_, 4 * s - 12 + kk_), acc);
+      for (int g = 0; g < GI; ++g) acc[g] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 10; ++s) {
+        const double bs = sg_coef(sgs, nF_, li_, 4 * s - 12 + kk_);
+#pragma unroll
+        for (int g = 0; g < GI; ++g) acc[g] = mfma_f64(x[s][g], bs, acc[g]);
+      }
       store(acc, 0, min(kMfV, fl_));
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -872,48 +881,58 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
         for (int i = 0; i < 4; ++i) nx[i] = tload(16 * t + 44 + 4 * i + kk_);
         // steps 4 t + 10 + i -> slot (4 (u + 1) + 10 + i) & 15  (t = t0 + u, t0 = 1 mod 4)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) x[(4 * (u + 1) + 10 + i) & 15] = tfinish(pd[i]);
-        doublex4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-#if DVH_FV_MF_EXP == 3
-        for (int s = 0; s < 10; ++s) acc[s & 3] += x[(4 * (u + 1) + s) & 15];
-#else
-        for (int s = 0; s < 10; ++s) acc = mfma_f64(x[(4 * (u + 1) + s) & 15], BINT(s), acc);
+        for (int i = 0; i < 4; ++i) {
+          tfinish(pd[i], x[(4 * (u + 1) + 10 + i) & 15]);
+#if DVH_FV_MF_PAIR
+          // two samples' corners in flight at a time: the next pair's LDS addresses wait on this pair
+          if (i == 1) asm volatile("" : "+v"(pd[2].base), "+v"(pd[3].base) : "v"(x[(4 * (u + 1) + 10) & 15][GI - 1]), "v"(x[(4 * (u + 1) + 11) & 15][GI - 1]));
 #endif
+        }
+        doublex4 acc[GI];
+#pragma unroll
+        for (int g = 0; g < GI; ++g) acc[g] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < 10; ++s) {
+          const double bs = bpad[boff + 4 * s];
+#pragma unroll
+          for (int g = 0; g < GI; ++g) {
+#if DVH_FV_MF_EXP == 3
+            acc[g][s & 3] += x[(4 * (u + 1) + s) & 15][g];
+#else
+            acc[g] = mfma_f64(x[(4 * (u + 1) + s) & 15][g], bs, acc[g]);
+#endif
+          }
+        }
         store(acc, kMfV * t, fl_);
 #pragma unroll
         for (int i = 0; i < 4; ++i) pd[i] = nx[i];
 #if DVH_FV_MF_SB
-        // one tile per scheduling region; the MFMAs interleaved with the finishing arithmetic
-        asm volatile("" ::"v"(x[(4 * (u + 1) + 10) & 15]), "v"(x[(4 * (u + 1) + 11) & 15]),
-                     "v"(x[(4 * (u + 1) + 12) & 15]), "v"(x[(4 * (u + 1) + 13) & 15]));
-#if DVH_FV_MF_IL
-#pragma unroll
-        for (int s = 0; s < 10; ++s) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, DVH_FV_MF_IL, 0);  // then VALU
-        }
-#endif
+        // one tile per scheduling region, its samples finished in it
+        asm volatile("" ::"v"(x[(4 * (u + 1) + 10) & 15][0]), "v"(x[(4 * (u + 1) + 11) & 15][0]),
+                     "v"(x[(4 * (u + 1) + 12) & 15][0]), "v"(x[(4 * (u + 1) + 13) & 15][0]));
         __builtin_amdgcn_sched_barrier(0);
 #endif
       }
     }
     launder();
     {  // last tile: rows nF - 16 .. nF - 1 (right fit), fresh samples in two groups of 5
-      doublex4 acc = {0.0, 0.0, 0.0, 0.0};
+      doublex4 acc[GI];
+#pragma unroll
+      for (int g = 0; g < GI; ++g) acc[g] = doublex4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < 10; ++s) {
         const int xi = fl_ - 12 + 4 * s + kk_;
-        const double xs = sample(xi);
-        acc = mfma_f64(xs, sg_coef(sgs, nF_, fl_ + li_, xi), acc);
-        if (s == 4) asm volatile("" : "+v"(kk_) : "v"(xs));
+        double xs[GI];
+        sample(xi, xs);
+        const double bs = sg_coef(sgs, nF_, fl_ + li_, xi);
+#pragma unroll
+        for (int g = 0; g < GI; ++g) acc[g] = mfma_f64(xs[g], bs, acc[g]);
+        if (s == 4) asm volatile("" : "+v"(kk_) : "v"(xs[0]));
       }
       store(acc, fl_, nF_);
     }
   }
 }
-
-#undef BINT
 
 // per-row L1 norms -> 1 / ||row||_1 (map_fv norm=True: data / norm(data, ord=1, axis=-1))
 __global__ __launch_bounds__(256) void row_l1_kernel(const float* __restrict__ data, int64_t b_stride,
@@ -1116,20 +1135,21 @@ DVH_API int dvh_disp_fv_mfma(const double* FK, int32_t B, int32_t n_kb, int32_t 
   if ((int64_t)n_kb * n_fb > 8192) return set_error(-4, "FK grid larger than 8192 bins");
   if ((int64_t)nF * nV > 0x7fffffff) return set_error(-4, "f-v grid larger than 2^31 points");
   if (B <= 0 || nV <= 0) return 0;
-  const int nfk = n_kb * n_fb, nbuf = (nfk + 31) & ~31;
-  const size_t lds = sizeof(double) * ((size_t)nbuf + (size_t)sgl * sgl + 64);
-  hipError_t e = hipFuncSetAttribute((const void*)fv_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  constexpr int GI = DVH_FV_MF_GI;
+  const size_t lds = fv_mfma_lds(GI, n_kb * n_fb);
+  hipError_t e = hipFuncSetAttribute((const void*)fv_mfma_kernel<GI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
   const int n_vb = (nV + kMfWaves * kMfV - 1) / (kMfWaves * kMfV);
-  if (G <= 0) {  // ~2 k blocks, at most 16 images each
+  if (G <= 0) {  // ~2 k blocks, at most 16 images each, a multiple of GI
     G = (int)(((int64_t)n_vb * B) / 2048);
-    G = G < 1 ? 1 : (G > 16 ? 16 : G);
+    G = G < GI ? GI : (G > 16 ? 16 : G);
   }
+  G = (G + GI - 1) / GI * GI;
   const int n_ig = (B + G - 1) / G;
   const int xcd_map = (n_vb % 8 == 0) ? 1 : 0;
   const int64_t n_blk = (int64_t)n_vb * n_ig;
   if (n_blk > 0x7fffffff) return set_error(-4, "grid too large");
-  hipLaunchKernelGGL(fv_mfma_kernel, dim3((unsigned)n_blk), dim3(kMfWaves * 64), lds, (hipStream_t)stream, FK, B, G,
+  hipLaunchKernelGGL(fv_mfma_kernel<GI>, dim3((unsigned)n_blk), dim3(kMfWaves * 64), lds, (hipStream_t)stream, FK, B, G,
                      n_kb, n_fb, (const double2*)hx, cb, nF, nV, (const double2*)fw, sg, fv, n_vb, xcd_map);
   return last_launch();
 }
