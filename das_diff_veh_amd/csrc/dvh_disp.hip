@@ -24,6 +24,8 @@
 namespace dvh {
 
 typedef double doublex4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
 
 // v_mfma_f64_16x16x4_f64 lane maps: A[i = l & 15][k = l >> 4], B[k = l >> 4][j = l & 15],
 // D[row = (l >> 4) + 4 r][col = l & 15] for r in [0, 4).
@@ -94,6 +96,93 @@ __global__ __launch_bounds__(64) void tdft_gemm_kernel(const float* __restrict__
         if (row < M && col < N)
           atomicAdd(C + (int64_t)row * N + col, acc[i][j][r] * (row_scale ? (double)row_scale[row] : 1.0));
       }
+}
+
+// 1b. The same GEMM with the twiddle operand staged in LDS and reused across the rows of a block:
+// a block (4 waves) owns 64 rows x kTdNT 16-column tiles; each wave 16 rows x all kTdNT tiles, so one A
+// operand (the gather samples, float4 loads: lane (i, q) holds rows i, k = k0 + 8 q + s for the chunk's
+// 8 k-steps s -- the same k permutation on both operands) feeds kTdNT MFMAs.  The block stages the
+// twiddle chunk W[k0 .. k0 + 32)[c0 .. c0 + 16 kTdNT) by LDS-DMA (16 B per lane) into a double buffer,
+// the next chunk's while this one is multiplied; chunk row 8 q + s sits in LDS row 4 s + q, so the four
+// lane groups of one B-operand read hit rows next to each other (other bank halves), not 8 rows apart
+// (the same banks; measured the same, 96-101 us either way).  No split-K: the tile is stored, not
+// accumulated.  512 gathers of 25 x 500: 176 -> 96 us against the split-K kernel (DVH_TDFT_ROWS=0).
+constexpr int kTdNT = 7;   // 16-column tiles per block (112 columns)
+constexpr int kTdKC = 32;  // k per chunk
+constexpr int kTdRows = 64;
+
+__global__ __launch_bounds__(256) void tdft_rows_kernel(const float* __restrict__ data, int64_t b_stride,
+                                                        int64_t ch_stride, int32_t nch, int32_t M, int32_t K,
+                                                        const double* __restrict__ W, int32_t N,
+                                                        const float* __restrict__ row_scale, double* __restrict__ C) {
+  extern __shared__ __attribute__((aligned(16))) double wsm[];  // [2][kTdKC][kTdNT * 16]
+  constexpr int NC = kTdNT * 16, CH = kTdKC * NC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * kTdRows + wave * 16, c0 = blockIdx.y * NC;
+  const int li = lane & 15, q = lane >> 4;
+  const int row = m0 + li;
+  const bool rok = row < M;
+  const float* rowp = data + (rok ? (int64_t)(row / nch) * b_stride + (int64_t)(row % nch) * ch_stride : 0);
+  const bool vec4 = ((b_stride | ch_stride) & 3) == 0 && (reinterpret_cast<uintptr_t>(data) & 15) == 0;
+  // LDS-DMA of twiddle chunk kc into buffer buf: doubles e = r * NC + c (linear), 2 per lane per piece
+  const int n_chunk = (K + kTdKC - 1) / kTdKC;
+  auto stage = [&](int kc, int buf) {
+    for (int p = wave; p < CH / 128; p += 4) {
+      const int e = p * 128 + 2 * lane;
+      const int rho = e / NC, c = e - rho * NC;
+      const int r = 8 * (rho & 3) + (rho >> 2);  // LDS row rho = 4 s + q holds chunk row k = 8 q + s
+      const int kr = min(kc * kTdKC + r, K - 1), cc = min(c0 + c, N - 2);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(W + (int64_t)kr * N + cc), (lds_void*)(wsm + buf * CH + p * 128), 16,
+                                       0, 0);
+    }
+  };
+  // A operand of chunk kc: a[s] = data[row][k0 + 8 q + s] (0 past K or M)
+  auto load_a = [&](int kc, double (&a)[8]) {
+    const int kb = kc * kTdKC + 8 * q;
+    if (vec4 && kb + 8 <= K && rok) {
+      const float4 u = *reinterpret_cast<const float4*>(rowp + kb);
+      const float4 v = *reinterpret_cast<const float4*>(rowp + kb + 4);
+      a[0] = u.x; a[1] = u.y; a[2] = u.z; a[3] = u.w; a[4] = v.x; a[5] = v.y; a[6] = v.z; a[7] = v.w;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) a[s] = (rok && kb + s < K) ? (double)rowp[kb + s] : 0.0;
+    }
+  };
+  doublex4 acc[kTdNT];
+#pragma unroll
+  for (int t = 0; t < kTdNT; ++t) acc[t] = doublex4{0.0, 0.0, 0.0, 0.0};
+  double a[8];
+  stage(0, 0);
+  load_a(0, a);
+  for (int kc = 0; kc < n_chunk; ++kc) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's twiddles have landed (and a)
+    __syncthreads();  // ... for every wave; the other buffer's last readers are done
+    double an[8];
+    if (kc + 1 < n_chunk) {
+      stage(kc + 1, (kc + 1) & 1);
+      load_a(kc + 1, an);
+    }
+    // rows beyond K in a partial chunk multiply a = 0 with finite (clamped) twiddles
+    const double* Wc = wsm + (kc & 1) * CH;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+#pragma unroll
+      for (int t = 0; t < kTdNT; ++t) acc[t] = mfma_f64(a[s], Wc[(4 * s + q) * NC + t * 16 + li], acc[t]);
+    }
+    if (kc + 1 < n_chunk) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) a[s] = an[s];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < kTdNT; ++t) {
+    const int col = c0 + t * 16 + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = m0 + q + 4 * r;
+      if (rr < M && col < N) C[(int64_t)rr * N + col] = acc[t][r] * (row_scale ? (double)row_scale[rr] : 1.0);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -681,13 +770,14 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 #ifndef DVH_FV_MF_PAIR
 #define DVH_FV_MF_PAIR 0  // 1: finish the 4 new samples of a tile two at a time (fewer registers; 700 vs 684 us)
 #endif
+#ifndef DVH_FV_MF_FWPF
+#define DVH_FV_MF_FWPF 0  // 1: the per-frequency weights fw loaded with the tables, a tile ahead
+#endif
 #ifndef DVH_FV_MF_EXP
 #define DVH_FV_MF_EXP 0  // timing experiments only (wrong results): 1 no stores, 2 no sampling, 3 no MFMA
 #endif
 constexpr int kMfV = 16;      // velocities per wave
 constexpr int kMfWaves = 4;   // waves per block
-typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(1))) void gbl_void;
 
 __device__ __forceinline__ double sg_coef(const double* sgs, int nF, int f, int xi) {
   constexpr int L = 2 * kSgPad + 1, half = kSgPad;
@@ -790,6 +880,9 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
     // tiles: the table loads (tload) one tile before the weights, corners and arithmetic (tfinish).
     struct Pend {
       double2 w;
+#if DVH_FV_MF_FWPF
+      double2 y;
+#endif
       int base, fc;
       bool in;
     };
@@ -804,6 +897,9 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
       const int qi = p.fc * nV_ + vc_;
       p.w = hx[qi];
       p.base = cb[qi];
+#if DVH_FV_MF_FWPF
+      p.y = fw[p.fc];
+#endif
       return p;
     };
     auto tfinish = [&](const Pend& p, double* xo) {
@@ -812,8 +908,12 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
       for (int g = 0; g < GI; ++g) xo[g] = (double)p.fc;
       return;
 #endif
+#if DVH_FV_MF_FWPF
+      const double2 y = p.y;
+#else
       const double2 y = fw[p.fc];  // per frequency: 16 lanes share it (an LDS copy measured slower: the
                                    // corner reads already load the LDS, 700 vs 673 us)
+#endif
       const int base = p.base;
 #pragma unroll
       for (int g = 0; g < GI; ++g) {
@@ -975,6 +1075,16 @@ DVH_API int dvh_disp_tdft(const float* data, int64_t b_stride, int64_t ch_stride
   if (!data || !wt || !D) return set_error(-2, "null pointer argument");
   const int M = B * nch, N = 2 * n_fb;
   if (M <= 0 || N <= 0) return 0;
+  static const int rows_env = getenv("DVH_TDFT_ROWS") ? atoi(getenv("DVH_TDFT_ROWS")) : 1;
+  if (rows_env && (reinterpret_cast<uintptr_t>(wt) & 15) == 0) {  // N = 2 n_fb is even: 16-byte twiddle pieces
+    const size_t lds = sizeof(double) * 2 * kTdKC * kTdNT * 16;
+    hipError_t e = hipFuncSetAttribute((const void*)tdft_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+    dim3 grid((M + kTdRows - 1) / kTdRows, (N + kTdNT * 16 - 1) / (kTdNT * 16));
+    hipLaunchKernelGGL(tdft_rows_kernel, grid, dim3(256), lds, (hipStream_t)stream, data, b_stride, ch_stride, nch, M,
+                       nt, wt, N, row_scale, D);
+    return last_launch();
+  }
   hipError_t e = hipMemsetAsync(D, 0, sizeof(double) * (size_t)M * N, (hipStream_t)stream);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
   const int tiles = ((M + kGT - 1) / kGT) * ((N + kGT - 1) / kGT);

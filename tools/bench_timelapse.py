@@ -4,7 +4,8 @@
 One step = the f-v images of B gathers (one day's stacks at B pivots, the [-200, 0] m rows of a
 49 x 500 gather: 25 channels x 500 lags) on a 512-velocity x 1,000-frequency grid (compute_disp_image
 -> Dispersion -> map_fv, modules/utils.py:383-426, 457-475), through the dispersion kernels:
-  tdft_gemm_kernel    time DFT as a real float64 MFMA GEMM [B*nch x nt] . [nt x 2*n_fb]
+  tdft_*_kernel       time DFT as a real float64 MFMA GEMM [B*nch x nt] . [nt x 2*n_fb] (tdft_rows_kernel:
+                      LDS-staged twiddles; the key "tdft_gemm_kernel" below is the time-DFT launch, either kernel)
   fk_contract_kernel  channel contraction, complex float64 MFMA GEMM per gather, |.|
   fv_*_kernel         FITPACK bilinear sampling + Savitzky-Golay(25, 4), float32 out (the product dispatch:
                       fv_mfma_kernel, the filter as banded float64 MFMA GEMMs, for a batch this size)
