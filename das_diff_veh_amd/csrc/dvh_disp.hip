@@ -770,6 +770,9 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 #ifndef DVH_FV_MF_PAIR
 #define DVH_FV_MF_PAIR 0  // 1: finish the 4 new samples of a tile two at a time (fewer registers; 700 vs 684 us)
 #endif
+#ifndef DVH_FV_MF_IL
+#define DVH_FV_MF_IL 0  // > 0: interleave each MFMA with this many VALU instructions (sched_group_barrier)
+#endif
 #ifndef DVH_FV_MF_FWPF
 #define DVH_FV_MF_FWPF 0  // 1: the per-frequency weights fw loaded with the tables, a tile ahead
 #endif
@@ -1010,6 +1013,15 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
         // one tile per scheduling region, its samples finished in it
         asm volatile("" ::"v"(x[(4 * (u + 1) + 10) & 15][0]), "v"(x[(4 * (u + 1) + 11) & 15][0]),
                      "v"(x[(4 * (u + 1) + 12) & 15][0]), "v"(x[(4 * (u + 1) + 13) & 15][0]));
+#if DVH_FV_MF_IL
+        // the tile's MFMAs spread through the sampling arithmetic: 1 MFMA, then IL VALU, then 1 LDS read
+#pragma unroll
+        for (int s = 0; s < 10 * GI; ++s) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, DVH_FV_MF_IL, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+#endif
         __builtin_amdgcn_sched_barrier(0);
 #endif
       }

@@ -12,7 +12,8 @@ TOL = 1e-4
 @pytest.mark.parametrize("mode", [None, ("DVH_FV_TILE", "2"), ("DVH_FV_TILE", "0"), ("DVH_FV_G", "3"),
                                   ("DVH_FV_G", "16"), ("DVH_FV_TG", "3"), ("DVH_FV_G", "0"), ("DVH_FV_CELLS", "1"),
                                   ("DVH_FV_CELLS", "0"), ("DVH_FV_MFMA", "1"), ("DVH_FV_MG", "3")])
-@pytest.mark.parametrize("B,nv,nf", [(40, 512, 1000), (7, 300, 242), (5, 64, 1001), (3, 61, 25), (4, 33, 413)])
+@pytest.mark.parametrize("B,nv,nf", [(40, 512, 1000), (7, 300, 242), (5, 64, 1001), (3, 61, 25), (4, 33, 413),
+                                     (3, 17, 32), (2, 16, 40), (5, 70, 47)])
 def test_fv_batch_vs_oracle(device, monkeypatch, B, nv, nf, mode):
     """mode: kernel selection read at each launch -- None = default dispatch, DVH_FV_TILE=2 -> always
     the frequency-tiled kernel, DVH_FV_TILE=0 -> batched / per-image dispatch, DVH_FV_G = images per block of the batched kernel (0: per-image
