@@ -17,7 +17,7 @@ then [N > 1: one all-reduce of the partial class stacks] and the f-v image of ev
 (compute_disp_image(end_x=0, start_x=-200): 1,000 velocities x 242 frequencies).  Only the windows
 and the trajectories are resident before the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload synth10k|weights|speeds|sliding]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload synth10k|weights|speeds|sliding|timelapse]
                     [--scaling weak|strong]
 
 weak (default): every rank images its own full job (value = N x the job per step).  strong: ONE job
@@ -27,6 +27,8 @@ weights (configs[1]): two pivots (700 m, 680 m) x 1,895 passes (heavy/mid/light 
 60 x 5,500 in ONE resident buffer, one launch of each kernel per step, 6 class images.
 sliding (configs[3]): 4,096-channel windows imaged at every pivot they cross (host O(C + J) unit
 tables, validity of the resident pool computed at ingest), see DESIGN.md.
+timelapse (configs[4]): batched f-v images of daily stacks (512 gathers x 512 velocities x 1,000
+frequencies per step and rank, no exchange: days shard over the ranks), value = f-v images/s.
 
 Prints ONE JSON line (rank 0).  `value` = vehicle-pass windows per second over all ranks.
 """
@@ -73,6 +75,11 @@ WORKLOADS = {
     "speeds": dict(kind="resident", config="configs[0]-shape", pivots=[(700.0, 500.0, 900.0, (330, 1442, 336))],
                    n_ch=60, n_t=5500, gen_chunk=64, track_half=350,
                    desc="configs[0]-shape: 700_speeds, fast/mid/slow 330/1442/336, 60 ch x 5500"),
+    "timelapse": dict(kind="timelapse", config="configs[4]", B=512, nch=25, nt=500, nV=512, nF=1000,
+                      desc="configs[4]: time-lapse daily stacks, the f-v image (512 velocities x 1,000 frequencies, "
+                           "1-25 Hz, 200-1200 m/s) of 512 gathers of 25 ch x 500 lags per step and rank (a day's "
+                           "stacks at 512 pivots): time DFT + channel contraction on the fp64 MFMA pipe, FITPACK "
+                           "bilinear + Savitzky-Golay (fp64 MFMA); every rank images its own days"),
     "sliding": dict(kind="sliding", config="configs[3]", n_total=12544, n_ch=4096, n_t=8192, pool=256, pivot_every=8,
                     half_aperture=200.0, gen_chunk=2, merge=49,
                     desc="configs[3]: synthetic passes x 4096 ch x 8192, sliding pivots every 8 channels (+-200 m, "
@@ -447,6 +454,132 @@ def pmc_lookup(kernel, layout, key):
     return None, "no committed PMC summary with this launch layout"
 
 
+FP64_MFMA_PEAK_TF = 78.6  # MI355X FP64 matrix (dense), the f-v / DFT GEMMs' pipe
+
+
+def timelapse_main(args, world, rank, device):
+    """configs[4]: one step = the f-v images of B resident gathers (tdft + fk contraction + f-v kernels,
+    the product dispatch).  Days shard over the ranks with no data-path collective (weak scaling).
+    Roofline of the dominant kernel (the MFMA f-v kernel): float64 MFMA FLOPs it issues per launch / the
+    launch's HIP-event time on its stream, and the HBM fraction of the f-v bytes it writes."""
+    from das_diff_veh_amd import _lib
+    from das_diff_veh_amd.disp import _use_mfma
+    from das_diff_veh_amd.synth import synth_gathers
+    wl = WORKLOADS["timelapse"]
+    B, nch, nt = wl["B"], wl["nch"], wl["nt"]
+    dx, dt = 8.16, 0.003999999999997783
+    freqs, vels = np.linspace(1.0, 25.0, wl["nF"]), np.linspace(200.0, 1200.0, wl["nV"])
+    t0 = time.time()
+    plan = DispPlan(nch, nt, dx, dt, freqs, vels)
+    data = synth_gathers(B, nch, nt, dx, dt, device, seed=1000 + rank)
+    tb = plan.tables(device)
+    st = _lib.stream_of(device)
+    stream = torch.cuda.current_stream(device)
+    D = torch.empty((B * nch, 2 * plan.n_fb), dtype=torch.float64, device=device)
+    FK = torch.empty((B, plan.n_kb, plan.n_fb), dtype=torch.float64, device=device)
+    fv = torch.empty((B, plan.nV, plan.nF), dtype=torch.float32, device=device)
+    t_setup = time.time() - t0
+
+    def run(ev=None):
+        if ev:
+            ev[0].record(stream)
+        _lib.call("dvh_disp_tdft", _lib.ptr(data), data.stride(0), data.stride(1), B, nch, nt, _lib.ptr(tb["wt"]),
+                  plan.n_fb, None, _lib.ptr(D), st)
+        if ev:
+            ev[1].record(stream)
+        _lib.call("dvh_disp_fk", _lib.ptr(D), B, nch, plan.n_fb, _lib.ptr(tb["atab"]), plan.MT, plan.K2, plan.n_kb,
+                  _lib.ptr(FK), None, None, st)
+        if ev:
+            ev[2].record(stream)
+        fv_from_fk(FK, plan, out=fv)
+        if ev:
+            ev[3].record(stream)
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        run(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = max_over_ranks(elapsed, device)
+    t = np.array([[e[i].elapsed_time(e[i + 1]) for i in range(3)] for e in evs]).mean(axis=0) / 1e3  # s
+
+    # parity: two images against the oracle (after timing)
+    from oracle import disp as odisp
+    host = data.double().cpu().numpy()
+    errs, picks = [], []
+    for b in (0, B - 1):
+        ref = odisp.map_fv(host[b], dx, dt, freqs, vels)
+        got = fv[b].double().cpu().numpy()
+        errs.append(float(np.abs(got - ref).max() / np.abs(ref).max()))
+        picks.append(bool(np.all(odisp.pick_ok(ref, got.argmax(axis=0)))))
+
+    mfma = _use_mfma(plan, B)
+    n_tiles = -(-(plan.nF - 16) // 16) + 1
+    mfma_flop = 2.0 * 16 * 16 * 40 * n_tiles * B * -(-plan.nV // 16)  # 10 v_mfma_f64_16x16x4 per 16 x 16 tile
+    fv_bytes = 4.0 * B * plan.nV * plan.nF + 8.0 * B * plan.n_kb * plan.n_fb
+    tdft_flop = 2.0 * B * nch * nt * 2 * plan.n_fb
+    traffic, traffic_src = None, "no committed time-lapse PMC summary"
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary_timelapse.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        k = d.get("fv_mfma_kernel")
+        if mfma and k and "traffic_bytes" in k and (B, plan.nV, plan.nF) == (512, 512, 1000):
+            traffic, traffic_src = float(k["traffic_bytes"]), os.path.basename(f)  # tools/pmc_timelapse.sh: same shape
+            break
+    achieved = (mfma_flop if mfma else 2.0 * 25 * B * plan.nV * plan.nF) / t[2] / 1e12
+    res = {
+        "metric": "time-lapse f-v images/sec (configs[4]: 512 velocities x 1,000 frequencies per image); % MFMA roofline",
+        "value": world * B * args.steps / elapsed, "unit": "f-v images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64 (DFT, contraction, FIR on the MFMA pipe), f32 images",
+        "data": "synthetic dispersive gathers (c(f) = 250 + 4000 / (f + 4) m/s + noise), resident",
+        "config": {"workload": "timelapse", "baseline_config": wl["config"], "description": wl["desc"],
+                   "gathers_per_step_this_rank": B, "nch": nch, "nt": nt, "nV": plan.nV, "nF": plan.nF,
+                   "parallelism": f"dp{world} (days sharded, no exchange)"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": "fv_mfma_kernel" if mfma else "fv_tile_kernel", "launch_ms": t[2] * 1e3,
+                     "flop_model": "10 v_mfma_f64_16x16x4_f64 per (16 velocities x 16 frequencies) tile, "
+                                   "ceil((nF - 16) / 16) + 1 tiles per row" if mfma else "25-tap FIR",
+                     "hbm_bytes_per_launch": fv_bytes, "hbm_frac": fv_bytes / t[2] / 1e9 / HBM_PEAK_GBS},
+        "kernels_ms": {"time_dft": t[0] * 1e3, "fk_contract": t[1] * 1e3, "fv": t[2] * 1e3},
+        "time_dft_mfma_frac": tdft_flop / t[0] / 1e12 / FP64_MFMA_PEAK_TF,
+        "parity": {"max_rel_err": max(errs), "picks_ok": all(picks), "images_checked": 2, "tol": 1e-4},
+        "host_setup_s": t_setup,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the oracle's map_fv (fft2, FITPACK bilinear via RectBivariateSpline, savgol) on one core over a
+        # bounded sample of the same gathers
+        budget = args.cpu_budget / 2
+        torch.set_num_threads(1)
+        n, t_c = 0, time.time()
+        while time.time() - t_c < budget and n < B:
+            odisp.map_fv(host[n], dx, dt, freqs, vels)
+            n += 1
+        secs = time.time() - t_c
+        res["cpu_baseline"] = {"value": n / secs, "unit": "f-v images/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/disp.py map_fv on {n} of the bench gathers in {secs:.1f} s, one core, "
+                                         f"cpu={platform.processor() or platform.machine()}"}
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -477,6 +610,8 @@ def main():
         backend = os.environ.get("DVH_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
 
+    if WORKLOADS[args.workload]["kind"] == "timelapse":
+        return timelapse_main(args, world, rank, device)
     if args.sliding_merge is not None:
         WORKLOADS["sliding"]["merge"] = args.sliding_merge
     job = build(args.workload, device, world, rank, args.scaling, chunk=args.chunk)
