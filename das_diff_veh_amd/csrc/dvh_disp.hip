@@ -764,21 +764,6 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 #ifndef DVH_FV_MF_WPE
 #define DVH_FV_MF_WPE (DVH_FV_MF_GI == 1 ? 3 : 2)  // waves per SIMD the kernel is register-budgeted for
 #endif
-#ifndef DVH_FV_MF_SB
-#define DVH_FV_MF_SB 1  // 1: one scheduling region per tile in the MFMA f-v kernel (0: the compiler's schedule)
-#endif
-#ifndef DVH_FV_MF_PAIR
-#define DVH_FV_MF_PAIR 0  // 1: finish the 4 new samples of a tile two at a time (fewer registers; 700 vs 684 us)
-#endif
-#ifndef DVH_FV_MF_IL
-#define DVH_FV_MF_IL 0  // > 0: interleave each MFMA with this many VALU instructions (sched_group_barrier)
-#endif
-#ifndef DVH_FV_MF_FWPF
-#define DVH_FV_MF_FWPF 0  // 1: the per-frequency weights fw loaded with the tables, a tile ahead
-#endif
-#ifndef DVH_FV_MF_EXP
-#define DVH_FV_MF_EXP 0  // timing experiments only (wrong results): 1 no stores, 2 no sampling, 3 no MFMA
-#endif
 constexpr int kMfV = 16;      // velocities per wave
 constexpr int kMfWaves = 4;   // waves per block
 
@@ -883,9 +868,6 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
     // tiles: the table loads (tload) one tile before the weights, corners and arithmetic (tfinish).
     struct Pend {
       double2 w;
-#if DVH_FV_MF_FWPF
-      double2 y;
-#endif
       int base, fc;
       bool in;
     };
@@ -893,30 +875,14 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
       Pend p;
       p.in = vok_ && f >= 0 && f < nF_;
       p.fc = min(max(f, 0), nF_ - 1);
-#if DVH_FV_MF_EXP == 2
-      p.w = {0.0, 0.0}; p.base = 0;
-      return p;
-#endif
       const int qi = p.fc * nV_ + vc_;
       p.w = hx[qi];
       p.base = cb[qi];
-#if DVH_FV_MF_FWPF
-      p.y = fw[p.fc];
-#endif
       return p;
     };
     auto tfinish = [&](const Pend& p, double* xo) {
-#if DVH_FV_MF_EXP == 2
-#pragma unroll
-      for (int g = 0; g < GI; ++g) xo[g] = (double)p.fc;
-      return;
-#endif
-#if DVH_FV_MF_FWPF
-      const double2 y = p.y;
-#else
       const double2 y = fw[p.fc];  // per frequency: 16 lanes share it (an LDS copy measured slower: the
                                    // corner reads already load the LDS, 700 vs 673 us)
-#endif
       const int base = p.base;
 #pragma unroll
       for (int g = 0; g < GI; ++g) {
@@ -934,9 +900,6 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
 #pragma unroll
       for (int g = 0; g < GI; ++g) {
         if (g >= ng) break;
-#if DVH_FV_MF_EXP == 1
-        if (acc[g][0] != 1.2345e300) return;
-#endif
         float* out_b = fv + (int64_t)(b0 + it + g) * nV_ * nF_;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -986,10 +949,6 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           tfinish(pd[i], x[(4 * (u + 1) + 10 + i) & 15]);
-#if DVH_FV_MF_PAIR
-          // two samples' corners in flight at a time: the next pair's LDS addresses wait on this pair
-          if (i == 1) asm volatile("" : "+v"(pd[2].base), "+v"(pd[3].base) : "v"(x[(4 * (u + 1) + 10) & 15][GI - 1]), "v"(x[(4 * (u + 1) + 11) & 15][GI - 1]));
-#endif
         }
         doublex4 acc[GI];
 #pragma unroll
@@ -999,31 +958,16 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
           const double bs = bpad[boff + 4 * s];
 #pragma unroll
           for (int g = 0; g < GI; ++g) {
-#if DVH_FV_MF_EXP == 3
-            acc[g][s & 3] += x[(4 * (u + 1) + s) & 15][g];
-#else
             acc[g] = mfma_f64(x[(4 * (u + 1) + s) & 15][g], bs, acc[g]);
-#endif
           }
         }
         store(acc, kMfV * t, fl_);
 #pragma unroll
         for (int i = 0; i < 4; ++i) pd[i] = nx[i];
-#if DVH_FV_MF_SB
         // one tile per scheduling region, its samples finished in it
         asm volatile("" ::"v"(x[(4 * (u + 1) + 10) & 15][0]), "v"(x[(4 * (u + 1) + 11) & 15][0]),
                      "v"(x[(4 * (u + 1) + 12) & 15][0]), "v"(x[(4 * (u + 1) + 13) & 15][0]));
-#if DVH_FV_MF_IL
-        // the tile's MFMAs spread through the sampling arithmetic: 1 MFMA, then IL VALU, then 1 LDS read
-#pragma unroll
-        for (int s = 0; s < 10 * GI; ++s) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, DVH_FV_MF_IL, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-#endif
         __builtin_amdgcn_sched_barrier(0);
-#endif
       }
     }
     launder();
