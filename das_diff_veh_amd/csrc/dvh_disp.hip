@@ -883,11 +883,13 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
     auto tfinish = [&](const Pend& p, double* xo) {
       const double2 y = fw[p.fc];  // per frequency: 16 lanes share it (an LDS copy measured slower: the
                                    // corner reads already load the LDS, 700 vs 673 us)
-      const int base = p.base;
+      // the corner pairs are merged into ds_read2_b64 (8 LDS cycles against 2 + 2 for single reads, but
+      // four opaque single reads measured slower: 743-751 vs 731 us)
+      const int i00 = p.base, i01 = p.base + 1, i10 = p.base + n_fb, i11 = p.base + n_fb + 1;
 #pragma unroll
       for (int g = 0; g < GI; ++g) {
         const double* F = fks + g * nbuf;
-        const double z00 = F[base], z01 = F[base + 1], z10 = F[base + n_fb], z11 = F[base + n_fb + 1];
+        const double z00 = F[i00], z01 = F[i01], z10 = F[i10], z11 = F[i11];
         const double val = (double)(float)(z00 * p.w.x * y.x + z01 * p.w.x * y.y + z10 * p.w.y * y.x +
                                            z11 * p.w.y * y.y);
         xo[g] = p.in ? val : 0.0;

@@ -15,7 +15,8 @@
 #define DVH_NO_READ2 0
 #endif
 // One LDS complex read.  With DVH_NO_READ2 the index is made opaque so that the compiler cannot
-// pair reads into ds_read2_b64 (8 LDS cycles on gfx950 against 2 + 2 for two ds_read_b64).
+// pair reads into ds_read2_b64 (8 LDS cycles on gfx950 against 2 + 2 for two ds_read_b64); measured
+// slower on the stack kernels (synth10k launch 3.84 vs 3.62-3.73 ms, sliding 9.65 vs 9.22 ms), so off.
 __device__ __forceinline__ float2 lds_ld(const float2* p, int idx) {
 #if DVH_NO_READ2
   asm volatile("" : "+v"(idx));
