@@ -34,7 +34,7 @@ from das_diff_veh_amd.disp import DispPlan, fv_from_fk  # noqa: E402
 from das_diff_veh_amd.synth import synth_gathers  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip parameters
-FP64_MFMA_PEAK_TF = 78.6       # MI355X spec sheet, FP64 matrix (dense)
+FP64_MFMA_PEAK_TF = 47.8       # v_mfma_f64_16x16x4_f64 measured on the box (tools/calib/dp_pipes); spec sheet 78.6
 
 
 def main():
