@@ -2,7 +2,7 @@
 # headline bench with CPU baseline + rocprofv3 stats, time-lapse bench + stats + PMC, sliding bench.
 #     bash tools/gpu_r2ab.sh TAG
 set -o pipefail
-tag=${1:-r2e}
+tag=${1:-r2h}
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/ab_tests.log 2>&1; rc=$?
 echo gpu_tests=$rc; tail -2 gpurun_out/ab_tests.log
