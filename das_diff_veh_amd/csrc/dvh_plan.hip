@@ -27,7 +27,7 @@
 namespace dvh {
 namespace {
 
-constexpr int kGeomBlock = 256;
+constexpr int kGeomBlock = 1024;  // one row per thread at R = 1023: the rows' dependent-load chains run side by side
 
 // first index i in [0, n) with !(a[i] < v); n when every a[i] < v.  For an ascending a this is
 // searchsorted(a, v, 'left'); a NaN v gives 0.
@@ -41,16 +41,52 @@ __device__ __forceinline__ int lower_bound(const double* __restrict__ a, int n, 
   return lo;
 }
 
+// lower_bound for an ascending a, started from the index a straight line through (a[0], a[n-1])
+// predicts: the answer is checked against its definition (a[i-1] < v <= a[i]) with two loads, and
+// only a miss falls back to the bisection, narrowed to the side of the guess the answer lies on.
+// Same result as lower_bound for every ascending a (uniform axes and tracking grids hit the guess
+// or its neighbour, so the 13-step chain of dependent loads over an 8192-sample axis becomes 2-4).
+__device__ __forceinline__ int lower_bound_guess(const double* __restrict__ a, int n, double v) {
+  if (n <= 0) return 0;
+  const double a0 = a[0], a1 = a[n - 1];
+  double gd = (n > 1 && a1 > a0) ? (v - a0) / (a1 - a0) * (double)(n - 1) + 1.0 : 0.0;
+  if (!(gd >= 0.0)) gd = 0.0;  // NaN v lands here
+  if (gd > (double)n) gd = (double)n;
+  const int g = (int)gd;
+  const bool lo_ok = g == 0 || a[g - 1] < v;
+  const bool hi_ok = g == n || !(a[g] < v);
+  if (lo_ok && hi_ok) return g;
+  if (lo_ok) {  // a[g] < v: the answer is above g; try g + 1 before bisecting
+    if (g + 1 == n || !(a[g + 1] < v)) return g + 1;
+    int lo = g + 2, hi = n;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (a[mid] < v) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  }
+  // !(a[g-1] < v): the answer is at most g - 1
+  if (g - 1 == 0 || a[g - 2] < v) return g - 1;
+  int lo = 0, hi = g - 2;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
 // np.argmax(t >= v) for ascending t
 __device__ __forceinline__ int first_ge(const double* __restrict__ t, int n, double v) {
-  const int i = lower_bound(t, n, v);
+  const int i = lower_bound_guess(t, n, v);
   return i >= n ? 0 : i;
 }
 
 // interp1d(x, y, kind='linear', fill_value='extrapolate')(xq) for strictly ascending x, n >= 2
 __device__ __forceinline__ double interp_extrap(const double* __restrict__ x, const double* __restrict__ y, int n,
                                                 double xq) {
-  int i = lower_bound(x, n, xq);
+  int i = lower_bound_guess(x, n, xq);
   i = i < 1 ? 1 : (i > n - 1 ? n - 1 : i);
   const int lo = i - 1;
   const double slope = __ddiv_rn(__dsub_rn(y[i], y[lo]), __dsub_rn(x[i], x[lo]));
@@ -65,7 +101,7 @@ __device__ __forceinline__ int2 py_slice(int64_t a, int64_t b, int64_t n) {
 }
 
 // One block per pass: every thread evaluates f(pivot) (a handful of loads, identical result) and
-// then the rows i = tid, tid + 256, ...
+// then the rows i = tid, tid + kGeomBlock, ...
 __global__ __launch_bounds__(kGeomBlock) void pass_geometry_kernel(
     const double* __restrict__ x_axis, int64_t x_stride, const double* __restrict__ t_axis, int64_t t_stride,
     int32_t n_t, const double* __restrict__ trk_x, const double* __restrict__ trk_t, int64_t trk_stride,

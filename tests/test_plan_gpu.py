@@ -104,3 +104,30 @@ def test_bad_trajectory_status(device):
     assert np.array_equal(seg[0], seg[1])
     with pytest.raises(ValueError):
         dev.check()
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_irregular_axes_geometry(device, seed):
+    """Non-uniform t axes (jittered steps, a 20x-denser stretch, repeated samples) and trajectories
+    with uneven abscissa spacing, so the kernel's guessed search misses its first guess on both sides
+    and falls back to the narrowed bisection; the tables must still equal the host's."""
+    from das_diff_veh_amd.plan import VsgParams
+    rng = np.random.default_rng(seed)
+    n_pass, T = 12, 4096
+    from das_diff_veh_amd.synth import DT_W500
+    x_axis = np.sort(rng.uniform(0.0, 2000.0, size=256))
+    steps = 0.004 * rng.uniform(0.2, 1.8, size=(n_pass, T))
+    steps[:, 1000:1600] *= 0.05
+    steps[:, 2000:2010] = 0.0
+    # the first step sets dt (and w, nsamp) as in the reference: keep it the bench's exact 0.004
+    t_axis = np.empty((n_pass, T))
+    t_axis[:, :2] = DT_W500 + np.arange(2) * 0.004
+    t_axis[:, 2:] = t_axis[:, 1:2] + np.cumsum(steps[:, 2:], axis=1)
+    trks = []
+    for p in range(n_pass):
+        xs = np.sort(rng.choice(np.arange(-200.0, 2200.0, 0.5), size=400, replace=False))
+        v = rng.uniform(12.0, 30.0)
+        tc = t_axis[p, rng.integers(T // 4, 3 * T // 4)]
+        trks.append((xs, tc + (xs - 1000.0) / v + 0.05 * np.sin(xs / 37.0)))
+    prm = VsgParams(pivot=1000.0, start_x=300.0, end_x=1700.0, wlen=2, norm=False, include_other_side=True)
+    _compare(x_axis, t_axis, trks, prm, 256, device)
