@@ -511,6 +511,10 @@ constexpr int kScanDepth = DVH_SCAN_DEPTH;
 #ifndef DVH_SCAN_COMPLEMENT
 #define DVH_SCAN_COMPLEMENT 0  // skip the blocks the correlation waves validate
 #endif
+#ifndef DVH_SCAN_ORDER
+#define DVH_SCAN_ORDER 1  // scan the passes in the correlation's (class-sorted) order, not index order: 3.51 vs
+                          // 3.53 ms per synth10k launch (tools/gpu_r2aj.sh; allocating loads, AUX 0, lost 4 %)
+#endif
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
 
@@ -723,7 +727,8 @@ __device__ __forceinline__ uint32_t scan_unit_blocks(const VsgArgs& A, int p, in
 // list: this wave's LDS scratch of kScanListBytes.
 __device__ __forceinline__ void scan_units(const VsgArgs& A, int n_ch, int n_t, uint32_t* __restrict__ vflag,
                                            uint32_t* __restrict__ counter, uint32_t* __restrict__ list, int lane,
-                                           char* ring = nullptr, int ring_kib = 0) {
+                                           char* ring = nullptr, int ring_kib = 0,
+                                           const int32_t* __restrict__ sorder = nullptr) {
   const int upp = (n_ch + kScanRows - 1) / kScanRows;  // units per pass
   const int n_units = A.n_pass * upp;
   const bool vec = (n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
@@ -734,7 +739,8 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, int n_ch, int n_t, 
   int u = pull_unit(counter, lane);
   while (u < n_units) {
     const int un = pull_unit(counter, lane);  // the next unit's index, fetched under this unit's loads
-    const int p = u / upp, c0 = (u - p * upp) * kScanRows;
+    const int q = u / upp, c0 = (u - q * upp) * kScanRows;
+    const int p = sorder ? uni(sorder[q]) : q;
     const int c1 = min(c0 + kScanRows, n_ch);
     const uint32_t m = blocks ? scan_unit_blocks(A, p, c0, c1, n_ch, n_t, list, lane)
                               : scan_rows(A.win + (int64_t)p * A.pass_stride, A.ch_stride, c0, c1, n_t, vec, lane,
@@ -778,7 +784,12 @@ __global__ __launch_bounds__(64 * (kFft + kScan), 4) void vsg_stackv_kernel(
       ring_kib = DVH_SCAN_RING;
     }
   }
-  scan_units(A, n_ch, n_t, vflag, counter, DVH_SCAN_COMPLEMENT ? list : nullptr, lane, ring, ring_kib);
+  const int32_t* sorder = nullptr;
+#if DVH_SCAN_ORDER
+  // the chunks cover order[0, end of the last chunk): scan in that order when it lists every pass
+  if (n_chunk > 0 && uni(chunk_tab[3 * (n_chunk - 1) + 1]) == A.n_pass) sorder = order;
+#endif
+  scan_units(A, n_ch, n_t, vflag, counter, DVH_SCAN_COMPLEMENT ? list : nullptr, lane, ring, ring_kib, sorder);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
