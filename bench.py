@@ -160,16 +160,16 @@ def build_pool(wl, device, world, rank, scaling, chunk):
     trk_len = torch.full((n_loc,), xs.size, dtype=torch.int32, device=device)
     job.sumsq = torch.empty(pool, dtype=torch.float64, device=device)
     job.scales = torch.empty((pool, 2), dtype=torch.float32, device=device)
-    seg_buf = None
+    # the step's tables for all its passes in one geometry launch (10 240 blocks instead of 20 launches of
+    # 512); each batch's plan is a slice of it
+    job.plan_all = DevicePlan(x_axis, t_axis, trk_x, trk_t, trk_len, prm, n_ch, derive=False) if n_loc else None
     job.batches = []
     for b in range(0, n_loc, pool):
         sl = slice(b, min(b + pool, n_loc))
         nb = sl.stop - sl.start
-        plan = DevicePlan(x_axis, t_axis, trk_x[sl], trk_t[sl], trk_len[sl], prm, n_ch, derive=False,
-                          seg_out=seg_buf)
-        seg_buf = plan.seg_tab if seg_buf is None else seg_buf  # one table buffer for every batch
         sched = StackSchedule(slots[mine[sl]], 3, chunk=chunk, counts=counts)
-        job.batches.append(Batch(plan, sched, job.windows[:nb], job.sumsq[:nb], job.scales[:nb]))
+        job.batches.append(Batch(job.plan_all.slice(sl.start, sl.stop), sched, job.windows[:nb], job.sumsq[:nb],
+                                 job.scales[:nb], derive=False))
         job.batches[-1].slots = slots[mine[sl]]
     job.t_plan = time.time() - t0
     job.n_local, job.n_global = n_loc, (n_job if scaling == "strong" else n_job * world)
@@ -330,6 +330,8 @@ def step(job, world, ev=None, fused=True):
             ev[name][j][k].record()
     for j, b in enumerate(job.batches):
         mark("geometry", j, 0)
+        if j == 0 and getattr(job, "plan_all", None) is not None:
+            job.plan_all.derive()  # every batch's tables (the batches' plans are slices of it)
         if b.derive:
             b.plan.derive()
         mark("geometry", j, 1)
@@ -633,8 +635,8 @@ def main():
     for _ in range(args.warmup):
         step(job, world, fused=not args.separate_validity)
     torch.cuda.synchronize()
-    # algorithmic bytes of every stack launch (bookkeeping outside the timed region: the tables of
-    # the last derived batch are on the device; re-derive each and copy it back once)
+    # algorithmic bytes of every stack launch (bookkeeping outside the timed region: a batch whose
+    # tables share a buffer with others is re-derived first; each batch's tables are copied back once)
     fused = [bool(not args.separate_validity and b.validity and (b.plan.flags & 6)) for b in job.batches]
     corr_bytes, win_bytes = [], []
     out_bytes = 4 * job.stack.shape[0] * job.stack.shape[1] * job.stack.shape[2]

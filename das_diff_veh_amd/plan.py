@@ -329,6 +329,24 @@ class DevicePlan:
     def device_tables(self, device=None):
         return self.pass_tab, self.seg_tab
 
+    def slice(self, a, b):
+        """Passes [a, b) as a plan of their own whose tables are views of this plan's: one derive()
+        of the whole plan forms every slice's tables in a single launch (a pipeline's batches), and a
+        slice's derive() re-forms only its passes."""
+        import copy
+        if not 0 <= a < b <= self.n_pass:
+            raise ValueError(f"slice [{a}, {b}) outside the plan's {self.n_pass} passes")
+        sub = copy.copy(self)
+        sub.n_pass = b - a
+        for name in ("pass_tab", "pivot_x", "trk_x", "trk_t", "trk_len", "seg_tab", "status"):
+            setattr(sub, name, getattr(self, name)[a:b])
+        if self._x.dim() == 2:
+            sub._x = self._x[a:b]
+        if self._t.dim() == 2:
+            sub._t = self._t[a:b]
+        sub.geoms = None
+        return sub
+
     def check(self):
         """Raise like interp1d would for passes whose trajectory could not be evaluated (synchronises)."""
         bad = np.nonzero(self.status.cpu().numpy())[0]

@@ -131,3 +131,33 @@ def test_irregular_axes_geometry(device, seed):
         trks.append((xs, tc + (xs - 1000.0) / v + 0.05 * np.sin(xs / 37.0)))
     prm = VsgParams(pivot=1000.0, start_x=300.0, end_x=1700.0, wlen=2, norm=False, include_other_side=True)
     _compare(x_axis, t_axis, trks, prm, 256, device)
+
+
+def test_plan_slices_share_one_derive(device):
+    """DevicePlan.slice: one derive() of the whole plan gives every slice the tables its own
+    derive() forms (the bench derives a step's batches in one launch)."""
+    import torch
+
+    from das_diff_veh_amd.plan import DevicePlan, VsgParams, pack_trajectories
+    from das_diff_veh_amd.synth import DT_W500
+    x_axis = 0.37 + 8.16 * np.arange(1024)
+    t_axis = DT_W500 + np.arange(8192) * 0.004
+    prm = VsgParams(pivot=4178.0, start_x=0.0, end_x=8400.0, wlen=2, norm=False, include_other_side=True)
+    trks = synth10k_trajectories(x_axis, t_axis, 5, 37)
+    tx, tt, tl = pack_trajectories(trks, device)
+    whole = DevicePlan(x_axis, t_axis, tx, tt, tl, prm, 1024).check()
+    ref = whole.host_seg_tab().copy()
+    parts = [whole.slice(a, min(a + 16, 37)) for a in range(0, 37, 16)]
+    whole.seg_tab.fill_(-1)
+    whole.derive()
+    torch.cuda.synchronize()
+    assert np.array_equal(np.concatenate([p.host_seg_tab() for p in parts]), ref)
+    whole.seg_tab.fill_(-1)
+    for p in parts:
+        p.derive()
+    torch.cuda.synchronize()
+    assert np.array_equal(whole.host_seg_tab(), ref)
+    assert [p.n_pass for p in parts] == [16, 16, 5]
+    assert np.array_equal(parts[1].pass_tab.cpu().numpy(), whole.pass_tab.cpu().numpy()[16:32])
+    with pytest.raises(ValueError):
+        whole.slice(30, 40)
