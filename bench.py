@@ -159,7 +159,9 @@ def build_pool(wl, device, world, rank, scaling, chunk):
     trk_x = torch.from_numpy(xs).to(device).expand(n_loc, xs.size).contiguous()
     trk_len = torch.full((n_loc,), xs.size, dtype=torch.int32, device=device)
     job.sumsq = torch.empty(pool, dtype=torch.float64, device=device)
-    job.scales = torch.empty((pool, 2), dtype=torch.float32, device=device)
+    # a scale buffer per batch: the step forms every batch's scales up front, side by side on a few streams
+    job.scales = torch.empty((n_loc, 2), dtype=torch.float32, device=device)
+    job.side_streams = [torch.cuda.Stream(device=device) for _ in range(3)]
     # the step's tables for all its passes in one geometry launch (10 240 blocks instead of 20 launches of
     # 512); each batch's plan is a slice of it
     job.plan_all = DevicePlan(x_axis, t_axis, trk_x, trk_t, trk_len, prm, n_ch, derive=False) if n_loc else None
@@ -169,7 +171,7 @@ def build_pool(wl, device, world, rank, scaling, chunk):
         nb = sl.stop - sl.start
         sched = StackSchedule(slots[mine[sl]], 3, chunk=chunk, counts=counts)
         job.batches.append(Batch(job.plan_all.slice(sl.start, sl.stop), sched, job.windows[:nb], job.sumsq[:nb],
-                                 job.scales[:nb], derive=False))
+                                 job.scales[sl], derive=False))
         job.batches[-1].slots = slots[mine[sl]]
     job.t_plan = time.time() - t0
     job.n_local, job.n_global = n_loc, (n_job if scaling == "strong" else n_job * world)
@@ -328,6 +330,36 @@ def step(job, world, ev=None, fused=True):
     def mark(name, j, k):
         if ev is not None:
             ev[name][j][k].record()
+    side = getattr(job, "side_streams", None)
+    if side and fused and all(b.validity and (b.plan.flags & 6) and not b.derive for b in job.batches):
+        # every batch's tables in one launch, then every batch's scales (one wave per pass, latency bound)
+        # spread over the main and side streams so they run side by side, then the stack launches
+        main = torch.cuda.current_stream()
+        mark("geometry", 0, 0)
+        job.plan_all.derive()
+        mark("geometry", 0, 1)
+        streams = [main] + side
+        for st in side:
+            st.wait_stream(main)
+        mark("scales", 0, 0)  # the phase is the main stream's wall time from the first scales to the join
+        for j, b in enumerate(job.batches):
+            with torch.cuda.stream(streams[j % len(streams)]):
+                vsg_scales(b.win, b.plan, out=b.scales, win_sumsq=None, validity=False)
+        for st in side:
+            main.wait_stream(st)
+        mark("scales", 0, 1)
+        for j, b in enumerate(job.batches):
+            for name in (("geometry", "validity", "scales") if j > 0 else ("validity",)):
+                mark(name, j, 0)
+                mark(name, j, 1)
+            mark("stack", j, 0)
+            vsg_stack_validated(b.win, b.plan, b.sched, scales=b.scales, out=job.stack, accumulate=j > 0, work=job.work)
+            mark("stack", j, 1)
+        if world > 1:
+            allreduce_stacks([job.stack])
+        a, e = job.disp_rows
+        fv_from_fk(fk_grid(job.stack[:, a:e, :], job.disp), job.disp, out=job.fv)
+        return
     for j, b in enumerate(job.batches):
         mark("geometry", j, 0)
         if j == 0 and getattr(job, "plan_all", None) is not None:
