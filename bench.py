@@ -18,11 +18,12 @@ then [N > 1: one all-reduce of the partial class stacks] and the f-v image of ev
 and the trajectories are resident before the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload synth10k|weights|speeds|sliding|timelapse]
-                    [--scaling weak|strong]
+                    [--scaling weak|strong|both]
 
-weak (default): every rank images its own full job (value = N x the job per step).  strong: ONE job
-of the configured size is split over the ranks (das_diff_veh_amd.distributed.shard_passes: every
-class dealt round robin), class means with the global counts, one all-reduce.
+weak (default at N = 1): every rank images its own full job (value = N x the job per step).  strong:
+ONE job of the configured size is split over the ranks (das_diff_veh_amd.distributed.shard_passes:
+every class dealt round robin), class means with the global counts, one all-reduce.  both (default at
+N > 1): the weak line, with the strong measurement of the same workload in its "strong_scaling" field.
 weights (configs[1]): two pivots (700 m, 680 m) x 1,895 passes (heavy/mid/light 103/1,058/734) of
 60 x 5,500 in ONE resident buffer, one launch of each kernel per step, 6 class images.
 sliding (configs[3]): 4,096-channel windows imaged at every pivot they cross (host O(C + J) unit
@@ -31,6 +32,11 @@ timelapse (configs[4]): batched f-v images of daily stacks (512 gathers x 512 ve
 frequencies per step and rank, no exchange: days shard over the ranks), value = f-v images/s.
 
 Prints ONE JSON line (rank 0).  `value` = vehicle-pass windows per second over all ranks.
+
+Multi-GPU: `python bench.py --gpus N` (N > 1) run without a launcher (no WORLD_SIZE in the environment)
+starts the N ranks itself, one process per GPU, before anything here imports torch or touches HIP
+(launch_ranks); under `torch.distributed.run --nproc-per-node N` every rank checks that the world
+size equals --gpus.
 """
 from __future__ import annotations
 
@@ -39,14 +45,84 @@ import glob
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="synth10k",
+                    choices=("synth10k", "weights", "speeds", "sliding", "timelapse"))
+    ap.add_argument("--scaling", default=None, choices=("weak", "strong", "both"),
+                    help="weak: every rank its own job; strong: one job split over the ranks; both (default for "
+                         "N > 1): the weak line with the strong (fixed-job) measurement beside it")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--chunk", type=int, default=8, help="passes per stack task (one wave, one gather row)")
+    ap.add_argument("--sliding-merge", type=int, default=None,
+                    help="sliding: batches of trajectories per stack launch (default: all 49 in one launch)")
+    ap.add_argument("--separate-validity", action="store_true",
+                    help="window_sumsq launch per batch instead of the validity scan inside the stack launch")
+    ap.add_argument("--layout-out", default=None, help="write the launch layout (JSON) for tools/pmc_summary.py")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="test hook: the ranks launch_ranks starts print their rank environment instead of benching")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv, n):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1), relay rank 0's output and
+    return the worst exit status.  Runs before torch is imported: this process never initialises HIP,
+    and it starts children instead of replacing itself (no exec after a GPU was touched)."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0, _ = procs[0].communicate()
+    sys.stdout.write(out0.decode())
+    sys.stdout.flush()
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"[bench] rank exit codes {rcs}", file=sys.stderr, flush=True)
+        return bad[0] if bad[0] > 0 else 1
+    return 0
+
+
+if __name__ == "__main__":
+    _ARGS = parse_args()
+    if "WORLD_SIZE" not in os.environ and _ARGS.gpus > 1:
+        sys.exit(launch_ranks(sys.argv[1:], _ARGS.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != _ARGS.gpus:
+        print(f"[bench] --gpus {_ARGS.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: one rank per GPU expected",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    if _ARGS.launch_dry_run:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                             "MASTER_PORT")}), flush=True)
+        sys.exit(0)
+
+import numpy as np  # noqa: E402  (after the rank launch: the launching process never imports torch)
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
 sys.path.insert(0, ROOT)
 
 from das_diff_veh_amd.disp import DispPlan, fk_grid, fv_from_fk  # noqa: E402
@@ -463,9 +539,9 @@ def cpu_baseline(job, budget_s=20.0, workers=None):
                 value_1core=rate1)
 
 
-def layout_of(job, args):
+def layout_of(job, args, scaling):
     """What one profiled launch of the stack kernel covers (PMC counters are per launch)."""
-    return {"workload": args.workload, "chunk": args.chunk, "scaling": args.scaling,
+    return {"workload": args.workload, "chunk": args.chunk, "scaling": scaling,
             "validity": "separate" if args.separate_validity else "fused",
             "passes_per_launch": [int(b.plan.n_pass) for b in job.batches][:1],
             "launches_per_step": len(job.batches)}
@@ -526,7 +602,7 @@ def timelapse_main(args, world, rank, device):
         if ev:
             ev[1].record(stream)
         _lib.call("dvh_disp_fk", _lib.ptr(D), B, nch, plan.n_fb, _lib.ptr(tb["atab"]), plan.MT, plan.K2, plan.n_kb,
-                  _lib.ptr(FK), None, None, st)
+                  _lib.ptr(FK), None, None, 0, st)
         if ev:
             ev[2].record(stream)
         fv_from_fk(FK, plan, out=fv)
@@ -622,22 +698,7 @@ def timelapse_main(args, world, rank, device):
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="synth10k", choices=sorted(WORKLOADS))
-    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--chunk", type=int, default=8, help="passes per stack task (one wave, one gather row)")
-    ap.add_argument("--sliding-merge", type=int, default=None,
-                    help="sliding: batches of trajectories per stack launch (default: all 49 in one launch)")
-    ap.add_argument("--separate-validity", action="store_true",
-                    help="window_sumsq launch per batch instead of the validity scan inside the stack launch")
-    ap.add_argument("--layout-out", default=None, help="write the launch layout (JSON) for tools/pmc_summary.py")
-    args = ap.parse_args()
-
+    args = _ARGS
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -650,19 +711,39 @@ def main():
         # several ranks on one GPU (RCCL refuses that), reducing through host copies
         backend = os.environ.get("DVH_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"[bench] world size {dist.get_world_size()} != --gpus {args.gpus}")
 
     if WORKLOADS[args.workload]["kind"] == "timelapse":
         return timelapse_main(args, world, rank, device)
     if args.sliding_merge is not None:
         WORKLOADS["sliding"]["merge"] = args.sliding_merge
-    job = build(args.workload, device, world, rank, args.scaling, chunk=args.chunk)
+    scaling = args.scaling or ("weak" if world == 1 else "both")
+    res = measure(args, "strong" if scaling == "strong" else "weak", world, rank, device,
+                  cpu=rank == 0 and world == 1 and not args.no_cpu_baseline)
+    if scaling == "both":
+        # the fixed job of the configured size split over the ranks, measured beside the weak line
+        strong = measure(args, "strong", world, rank, device, cpu=False)
+        res["strong_scaling"] = {k: strong[k] for k in ("value", "ms_per_step", "scaling")}
+        res["strong_scaling"].update({k: strong["config"][k] for k in ("windows_per_step", "windows_per_step_this_rank")})
+        res["strong_scaling"]["stack_launch_ms"] = strong["roofline"]["launch_ms"]
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def measure(args, scaling, world, rank, device, cpu):
+    """Build the workload's job for `scaling`, time args.steps steps after args.warmup, and return the
+    result record (rank 0's view, elapsed = max over ranks)."""
+    job = build(args.workload, device, world, rank, scaling, chunk=args.chunk)
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: {job.windows.shape[0]} resident windows generated in {job.t_gen:.2f}s, host setup "
         f"{job.t_plan:.2f}s; {job.n_local} passes per step on this rank ({job.units} units), "
         f"{len(job.batches)} batches, R = {job.batches[0].plan.R}")
     if args.layout_out and rank == 0:
         with open(args.layout_out, "w") as fh:
-            json.dump(layout_of(job, args), fh)
+            json.dump(layout_of(job, args, scaling), fh)
 
     for _ in range(args.warmup):
         step(job, world, fused=not args.separate_validity)
@@ -706,7 +787,7 @@ def main():
     bytes_per_launch = float(np.mean(bytes_stack))
     launch_s = float(ms["stack"].mean()) / 1e3
     achieved = bytes_per_launch / launch_s / 1e9
-    layout = layout_of(job, args)
+    layout = layout_of(job, args, scaling)
     kname = "vsg_stackv_kernel" if all(fused) else "vsg_stackf_kernel"
     traffic, traffic_src = pmc_lookup(kname, layout, "traffic_bytes")
     step_ms = elapsed / args.steps * 1e3
@@ -719,7 +800,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": step_ms,
         "higher_is_better": True,
-        "scaling": args.scaling,
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (device-generated dispersive moving-source wavefield, per-pass trajectories)",
@@ -754,16 +835,15 @@ def main():
                             "instr_per_launch": valu, "source": valu_src, "clock_assumed_ghz": 2.4,
                             "model": "wave64 VALU instruction = 2 cycles on a SIMD-32 (>= 2 waves per SIMD) at the "
                                      "2.4 GHz max clock"}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and job.cpu_sets:
+    if cpu and job.cpu_sets:
         cb = cpu_baseline(job, args.cpu_budget)
         res["cpu_baseline"] = cb
         res["speedup_vs_cpu"] = res["value"] / cb["value"]
     else:
         res["cpu_baseline"] = None
-    if rank == 0:
-        print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    del job
+    torch.cuda.empty_cache()
+    return res
 
 
 if __name__ == "__main__":

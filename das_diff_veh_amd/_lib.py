@@ -31,7 +31,7 @@ SIGNATURES = {
                                 _i32, _p, _p, _p, _p],
     "dvh_disp_row_l1": [_p, _i64, _i64, _i32, _i32, _i32, _p, _p],
     "dvh_disp_tdft": [_p, _i64, _i64, _i32, _i32, _i32, _p, _i32, _p, _p, _p],
-    "dvh_disp_fk": [_p, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _p],
+    "dvh_disp_fk": [_p, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _i32, _p],
     "dvh_disp_fv": [_p, _i32, _i32, _i32, _p, _f64, _f64, _p, _i32, _i32, _p, _p, _p, _i32, _p, _p],
     "dvh_disp_fv_cells": [_p, _i32, _i32, _i32, _p, _f64, _f64, _p, _i32, _i32, _p, _p, _i32, _i32, _i32, _i32, _i32,
                           _p, _p, _p, _p, _p],

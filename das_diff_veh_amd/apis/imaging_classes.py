@@ -106,11 +106,26 @@ class VirtualShotGathersFromWindows(ImagesFromWindows):
         the partial stack gives every rank the same ``avg_image``; ``shard`` lists this rank's passes.
         skip_failed=True: a pass whose geometry or trajectory cannot be formed is left out of the mean
         and reported in ``failed`` {window index: reason} instead of raising for the whole list
-        (engine.stacked_checked); ``images`` then holds the imaged windows' gathers."""
+        (engine.stacked_checked); ``images`` then holds the imaged windows' gathers.  Both flags: the
+        passes every rank rejects alike are left out, the rest sharded (``shard`` in window indices)."""
         windows = list(self.windows)
         include_other_side = imaging_kwargs.pop("include_other_side", False)
         prm = vsg_params(include_other_side, norm=False, **imaging_kwargs)
         self.failed = {}
+        if skip_failed and shard_over_ranks:
+            # every rank holds the same list, so every rank rejects the same passes; the good ones are
+            # sharded and stacked with global counts over the imaged passes
+            self.failed, _ = engine.pass_failures(windows, prm)
+            good = [i for i in range(len(windows)) if i not in self.failed]
+            if not good:
+                raise ValueError(f"no pass could be imaged: {self.failed}")
+            stack, geoms, shard = engine.stacked_sharded([windows[i] for i in good], prm, group=group)
+            self.shard = [good[j] for j in shard]
+            self.images = _LazyGathers([windows[i] for i in good], prm)
+            avg = stack[0].detach().to("cpu").numpy().astype(np.float64)
+            self.avg_image = VirtualShotGather._from_arrays(windows[good[0]], avg, geoms[0].gather_x_axis,
+                                                            geoms[0].gather_t_axis)
+            return
         if skip_failed:
             stack, axes, self.failed = engine.stacked_checked(windows, prm)
             if stack is None:

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void fk_contract_kernel(const double* __restri
                                                            const double* __restrict__ Atab, int32_t MT, int32_t K2,
                                                            int32_t n_kb, double* __restrict__ FK,
                                                            const int32_t* __restrict__ slot,
-                                                           const float* __restrict__ weight) {
+                                                           const float* __restrict__ weight, int32_t n_slot) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int M2 = 2 * MT;
   double* Bs = sm;                      // [K2][kFN + 1]
@@ -236,7 +236,9 @@ __global__ __launch_bounds__(256) void fk_contract_kernel(const double* __restri
     if (q >= n_fb) continue;
     const double mag = hypot(Cs[m * (kFN + 1) + n], Cs[(MT + m) * (kFN + 1) + n]);
     if (slot) {
-      atomicAdd(FK + ((int64_t)slot[b] * n_kb + m) * n_fb + q, mag * (double)weight[b]);
+      const int sl = slot[b];
+      if (sl >= 0 && sl < n_slot)  // the host rejects such slots; never write outside FK
+        atomicAdd(FK + ((int64_t)sl * n_kb + m) * n_fb + q, mag * (double)weight[b]);
     } else {
       FK[((int64_t)b * n_kb + m) * n_fb + q] = mag;
     }
@@ -1060,9 +1062,10 @@ DVH_API int dvh_disp_tdft(const float* data, int64_t b_stride, int64_t ch_stride
 
 DVH_API int dvh_disp_fk(const double* D, int32_t B, int32_t nch, int32_t n_fb, const double* atab, int32_t MT,
                         int32_t K2, int32_t n_kb, double* FK, const int32_t* slot, const float* weight,
-                        void* stream) {
+                        int32_t n_slot, void* stream) {
   if (!D || !atab || !FK) return set_error(-2, "null pointer argument");
   if ((slot == nullptr) != (weight == nullptr)) return set_error(-2, "slot and weight go together");
+  if (slot && n_slot <= 0) return set_error(-2, "slot accumulation needs n_slot > 0");
   if (MT % 16 || n_kb > MT || K2 < 2 * nch || K2 % 4) return set_error(-2, "invalid contraction table shape");
   if (B <= 0 || n_fb <= 0) return 0;
   const size_t lds = sizeof(double) * ((size_t)K2 * (kFN + 1) + (size_t)2 * MT * (kFN + 1));
@@ -1072,7 +1075,7 @@ DVH_API int dvh_disp_fk(const double* D, int32_t B, int32_t nch, int32_t n_fb, c
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
   dim3 grid((n_fb + kFN - 1) / kFN, B);
   hipLaunchKernelGGL(fk_contract_kernel, grid, dim3(256), lds, (hipStream_t)stream, D, nch, n_fb, atab, MT, K2, n_kb,
-                     FK, slot, weight);
+                     FK, slot, weight, n_slot);
   return last_launch();
 }
 

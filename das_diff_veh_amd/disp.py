@@ -229,11 +229,14 @@ def fk_grid(data, plan: DispPlan, norm=False, slots=None, weights=None, n_slot=N
         FK = torch.empty((B, plan.n_kb, plan.n_fb), dtype=torch.float64, device=dev)
         sl = wt = None
     else:
+        slots = np.asarray(slots, dtype=np.int64)
+        if n_slot is None or slots.shape != (B,) or (B and (slots.min() < 0 or slots.max() >= n_slot)):
+            raise ValueError("fk_grid: one class slot in [0, n_slot) per gather")
         FK = torch.zeros((n_slot, plan.n_kb, plan.n_fb), dtype=torch.float64, device=dev)
-        sl = torch.as_tensor(np.asarray(slots, dtype=np.int32), device=dev)
+        sl = torch.as_tensor(slots.astype(np.int32), device=dev)
         wt = torch.as_tensor(np.asarray(weights, dtype=np.float32), device=dev)
     _lib.call("dvh_disp_fk", _lib.ptr(D), B, plan.nch, plan.n_fb, _lib.ptr(tb["atab"]), plan.MT, plan.K2,
-              plan.n_kb, _lib.ptr(FK), _lib.ptr(sl), _lib.ptr(wt), st)
+              plan.n_kb, _lib.ptr(FK), _lib.ptr(sl), _lib.ptr(wt), 0 if n_slot is None else int(n_slot), st)
     return FK
 
 

@@ -74,15 +74,43 @@ def sharded_class_means(partial, slots, n_slot, group=None):
     all_reduce(SUM) of that tensor gives every rank the class means sum(images) / len(images)
     (apis/imaging_classes.py:106-107).  Returns (means, mine)."""
     slots = np.asarray(slots, dtype=np.int64)
+    if slots.size and (slots.min() < 0 or slots.max() >= n_slot):
+        raise ValueError("class slot out of range [0, n_slot)")  # same list on every rank: all raise
     world, rank = world_rank(group)
     counts = global_counts(slots, n_slot)
     mine = shard_passes(slots, world, rank).astype(np.int64)
     weights = 1.0 / counts[slots[mine]] if mine.size else np.zeros(0)
-    part = partial(mine, weights)
-    if part.shape[0] != n_slot:
-        raise ValueError("partial() must return per-slot sums [n_slot, ...]")
+    # a pass only its owner images can fail (a trajectory interp1d rejects, a mute table, ...): every rank
+    # learns of it before the data all-reduce, so no rank is left waiting in the collective
+    err = None
+    try:
+        part = partial(mine, weights)
+        if part.shape[0] != n_slot:
+            raise ValueError("partial() must return per-slot sums [n_slot, ...]")
+    except Exception as e:  # noqa: BLE001 -- re-raised below, on this rank and (as a RuntimeError) on the others
+        err = e
+    failed = any_rank_failed(err is not None, group)
+    if err is not None:
+        raise err
+    if failed:
+        raise RuntimeError(f"sharded imaging failed on another rank (rank {failed - 1}); see its error")
     allreduce_stacks([part], group)
     return part, mine
+
+
+def any_rank_failed(mine_failed, group=None):
+    """0 when no rank of the group failed, else 1 + the lowest failing rank (one small all-reduce)."""
+    world, rank = world_rank(group)
+    if world == 1:
+        return 1 if mine_failed else 0
+    dev = None
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    code = (world - rank) if mine_failed else 0  # MAX picks the lowest failing rank
+    t = torch.tensor([code], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    v = int(t.item())
+    return 0 if v == 0 else world - v + 1
 
 
 def max_over_ranks(value, device=None, group=None):

@@ -107,6 +107,12 @@ def stacked_sharded(windows, prm: VsgParams, slots=None, n_slot=1, group=None, d
     keys, axes = zip(*[_axes(w, prm) for w in windows]) if windows else ((), ())
     if len({k[:2] for k in keys}) != 1:
         raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
+    # every pass is checked on every rank before sharding, so a bad pass raises the same error everywhere
+    # instead of only on its owner (distributed.sharded_class_means also shares any error a rank hits)
+    failed, _ = pass_failures(windows, prm)
+    if failed:
+        i = min(failed)
+        raise ValueError(f"pass {i}: {failed[i]}")
     R, w = keys[0][:2]
     counts = np.bincount(slots, minlength=n_slot)
 

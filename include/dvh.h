@@ -115,9 +115,10 @@ int dvh_disp_tdft(const float* data, int64_t b_stride, int64_t ch_stride, int32_
                   const double* wt, int32_t n_fb, const float* row_scale, double* D, void* stream);
 
 /* Channel contraction (complex GEMM on MFMA) + |.|: FK[B][n_kb][n_fb]; with slot/weight
- * (both non-NULL) FK[slot[b]] += weight[b] * |Z_b| instead (class mean of |FK|). */
+ * (both non-NULL) FK[slot[b]] += weight[b] * |Z_b| instead (class mean of |FK|), FK holding n_slot
+ * slots (a slot outside [0, n_slot) is never written; callers validate slots on the host). */
 int dvh_disp_fk(const double* D, int32_t B, int32_t nch, int32_t n_fb, const double* atab, int32_t MT, int32_t K2,
-                int32_t n_kb, double* FK, const int32_t* slot, const float* weight, void* stream);
+                int32_t n_kb, double* FK, const int32_t* slot, const float* weight, int32_t n_slot, void* stream);
 
 /* f-v sampling: fv[B][nV][nF] = savgol(float32(bilinear(FK; k = kq[f][v], f)))  with the
  * interp2d query order (kq sorted per frequency), FITPACK clamping to [kmin, kmax], the compact

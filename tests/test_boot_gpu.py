@@ -92,26 +92,30 @@ def test_resample_stacks_and_images(device):
         assert np.abs(fv[b] - rfv).max() <= 1e-4 * np.abs(rfv).max()
 
 
-def _pick_parity(dev_picks, ref_picks, ref_fv_band, vels, tol):
+def _pick_parity(dev_picks, ref_picks, ref_fv_band, dev_fv_band, vels):
     """Raw ridge picks (one velocity per band column): the device's must equal the reference's in every
-    column, except where the reference's own f-v column holds the device's pick within ``tol`` of its
-    maximum (a near-tie at the f-v parity bound, which either pick may win).  Returns the tie columns."""
+    column, except at a float tie the two images' own measured discrepancy allows: the device's pick is
+    accepted where the reference's f-v column holds it within 2 x max|device - reference| of that column
+    (both values of the pair may be off by that much) plus one float32 spacing of the column's values.
+    Returns the indices of the differing columns (the caller reports and bounds their count)."""
     vel_desc = np.asarray(vels, dtype=np.float64)[::-1]
-    ties = []
+    diff = []
     for i in np.flatnonzero(dev_picks != ref_picks):
         rd = int(np.flatnonzero(vel_desc == dev_picks[i])[0])
         rr = int(np.flatnonzero(vel_desc == ref_picks[i])[0])
         col = ref_fv_band[:, i].astype(np.float64)
-        assert abs(col[rd] - col[rr]) <= tol, (i, dev_picks[i], ref_picks[i], col[rd], col[rr])
-        ties.append(i)
-    return ties
+        err = float(np.abs(dev_fv_band[:, i].astype(np.float64) - col).max())
+        tol = 2.0 * err + float(np.spacing(np.float32(np.abs(col).max())))
+        assert abs(col[rd] - col[rr]) <= tol, (i, dev_picks[i], ref_picks[i], col[rd], col[rr], err)
+        diff.append(i)
+    return diff
 
 
 def test_bootstrap_disp_matches_reference(device):
     """Same draws as the reference (random.seed).  Per resample and mode: the ridge walk on our images
     equals the oracle's walk on the same images, and every raw pick equals the reference's pick on the
-    reference's own f-v map (tests/golden/ridge.npz:boot_fv) unless that column is a near-tie within the
-    f-v parity bound (rel 1e-4 of the image peak); with identical picks the smoothed ridges agree to 1e-9."""
+    reference's own f-v map (tests/golden/ridge.npz:boot_fv) unless that column is a float tie within the
+    two images' measured discrepancy (_pick_parity); with identical picks the smoothed ridges agree to 1e-9."""
     import torch
 
     from das_diff_veh_amd import bootstrap as bt
@@ -133,7 +137,6 @@ def test_bootstrap_disp_matches_reference(device):
     for b in range(4):
         ref_fv = g["boot_fv"][b]
         assert np.abs(fv[b] - ref_fv).max() <= 1e-4 * np.abs(ref_fv).max()
-        tol = 1e-4 * float(np.abs(ref_fv).max())
         for m, (lb, ub, ri, sg, vr, key) in enumerate(((2.5, 14, 80, 25, None, "boot_mode0"),
                                                        (10, 15, 130, 50, mode1, "boot_mode1"))):
             band = (fq >= lb) & (fq < ub)
@@ -147,17 +150,19 @@ def test_bootstrap_disp_matches_reference(device):
                               ref_vel=vr, return_picks=True)
             _, rp = orid.extract_ridge_ref_idx(fq[band], bt.VELS, ref_fv[:, band], ref_freq_idx=ref_idx, sigma=sg,
                                                vel_max=800, ref_vel=vr, return_picks=True)
-            ties = _pick_parity(dp[0], rp, ref_fv[:, band], bt.VELS, tol)
+            ties = _pick_parity(dp[0], rp, ref_fv[:, band], fv[b][:, band], bt.VELS)
             n_tie += len(ties)
             if not ties:
                 np.testing.assert_allclose(rv[m][b], g[key][b], rtol=0, atol=1e-9)
-    assert n_tie <= 2, n_tie  # near-ties are rare: at most a couple of columns over 8 ridges
+    print(f"differing raw picks (float ties within the measured f-v error): {n_tie} of 8 ridges")
+    assert n_tie <= 2, n_tie
 
 
 def test_convergence_test_small(device):
     """convergence_test (imaging_diff_speed.ipynb#cell30) for bt_size 1..3: each entry equals the summed
     std of the device ridges of the same draws (1e-9), and every raw pick of every resample equals the
-    reference-pinned oracle's pick on the oracle's own image (f64 VSG + map_fv) unless a near-tie; where
+    reference-pinned oracle's pick on the oracle's own image (f64 VSG + map_fv) unless a float tie within
+    the measured f-v error (_pick_parity); where
     a (bt_size, mode) has no tie the entry equals the oracle's to 1e-9."""
     from das_diff_veh_amd import bootstrap as bt
     from das_diff_veh_amd.apis.imaging_classes import convergence_test
@@ -192,9 +197,10 @@ def test_convergence_test_small(device):
             for b in range(4):
                 r, rp = orid.extract_ridge_ref_idx(fq[band], bt.VELS, ref_fv[b][:, band], ref_freq_idx=ref_idx,
                                                    sigma=sg, vel_max=800, ref_vel=vr, return_picks=True)
-                ties += len(_pick_parity(dp[b], rp, ref_fv[b][:, band], bt.VELS, 1e-4 * np.abs(ref_fv[b]).max()))
+                ties += len(_pick_parity(dp[b], rp, ref_fv[b][:, band], fv_dev[b].cpu().numpy()[:, band], bt.VELS))
                 ref_sm.append(r)
             if not ties:
                 assert abs(np.sum(np.std(np.stack(ref_sm), axis=0)) - got[m, k - 1]) <= 1e-9
             n_tie += ties
+    print(f"differing raw picks (float ties within the measured f-v error): {n_tie} over 24 ridges")
     assert n_tie <= 4, n_tie

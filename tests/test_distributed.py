@@ -79,3 +79,58 @@ def test_shard_balance():
     for s in range(3):
         per = [np.sum(slots[p] == s) for p in parts]
         assert max(per) - min(per) <= 1
+
+
+def _fail_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from das_diff_veh_amd.distributed import sharded_class_means
+        slots = np.array([0, 1, 0, 1, 0, 1])
+
+        def partial(mine, weights):
+            if 3 in mine.tolist():  # the pass only one rank owns is broken (e.g. a bad trajectory)
+                raise ValueError("pass 3: trajectory needs >= 2 distinct finite tracked points")
+            return torch.zeros((2, 4), dtype=torch.float64)
+
+        try:
+            sharded_class_means(partial, slots, 2)
+            q.put((rank, "no error"))
+        except ValueError as e:
+            q.put((rank, "ValueError: " + str(e)))
+        except RuntimeError as e:
+            q.put((rank, "RuntimeError: " + str(e)))
+        try:
+            sharded_class_means(partial, np.array([0, 2]), 2)  # slot out of range: every rank raises
+        except ValueError as e:
+            q.put((rank, "slot " + str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_error_on_one_rank_raises_on_every_rank():
+    """A pass that fails on the rank owning it must not leave the other ranks waiting in the all-reduce."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(4))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    msgs = {}
+    for r, m in out:
+        msgs.setdefault(r, []).append(m)
+    from das_diff_veh_amd.distributed import shard_passes
+    owner = 0 if 3 in shard_passes(np.array([0, 1, 0, 1, 0, 1]), 2, 0).tolist() else 1
+    assert any(m.startswith("ValueError: pass 3") for m in msgs[owner])
+    assert any(m.startswith("RuntimeError") for m in msgs[1 - owner])
+    for r in (0, 1):
+        assert any(m.startswith("slot class slot out of range") for m in msgs[r])

@@ -69,7 +69,7 @@ def main():
         if ev:
             ev[1].record(stream)
         _lib.call("dvh_disp_fk", _lib.ptr(D), B, nch, plan.n_fb, _lib.ptr(tb["atab"]), plan.MT, plan.K2, plan.n_kb,
-                  _lib.ptr(FK), None, None, st)
+                  _lib.ptr(FK), None, None, 0, st)
         if ev:
             ev[2].record(stream)
         fv_from_fk(FK, plan, out=fv)  # the product dispatch (cell-staged tiles for a batch this size)
