@@ -27,7 +27,7 @@ N > 1): the weak line, with the strong measurement of the same workload in its "
 weights (configs[1]): two pivots (700 m, 680 m) x 1,895 passes (heavy/mid/light 103/1,058/734) of
 60 x 5,500 in ONE resident buffer, one launch of each kernel per step, 6 class images.
 sliding (configs[3]): 4,096-channel windows imaged at every pivot they cross (host O(C + J) unit
-tables, validity of the resident pool computed at ingest), see DESIGN.md.
+tables); every pass's whole window validated inside the stack launch (134 MB per pass), see DESIGN.md.
 timelapse (configs[4]): batched f-v images of daily stacks (512 gathers x 512 velocities x 1,000
 frequencies per step and rank, no exchange: days shard over the ranks), value = f-v images/s.
 
@@ -159,9 +159,10 @@ WORKLOADS = {
     "sliding": dict(kind="sliding", config="configs[3]", n_total=12544, n_ch=4096, n_t=8192, pool=256, pivot_every=8,
                     half_aperture=200.0, gen_chunk=2, merge=49,
                     desc="configs[3]: synthetic passes x 4096 ch x 8192, sliding pivots every 8 channels (+-200 m, "
-                         "49 rows), each pass imaged at every pivot it crosses inside its window; 12,544 passes per "
-                         "GPU (100k over 8) as 49 batches over a resident pool of 256 windows; speed classes x "
-                         "pivots stacked, f-v image per (class, pivot)"),
+                         "49 rows), each pass imaged at every pivot it crosses inside its window and its whole window "
+                         "validated (||data||_F: NaN / inf / all zero); 12,544 passes per GPU (100k over 8) as 49 "
+                         "batches over a resident pool of 256 windows; speed classes x pivots stacked, f-v image per "
+                         "(class, pivot)"),
 }
 
 
@@ -327,12 +328,15 @@ def build_sliding(wl, device, world, rank, scaling, chunk):
     """configs[3]: a pool of long-fiber windows imaged at sliding pivots (UnitPlan, host tables).
 
     Every batch gives the pool new per-pass trajectories (crossing point uniform along the fiber,
-    15-30 m/s, crossing at mid-window); a pass becomes one unit per pivot it crosses inside its
-    window.  Slots = speed class x pivot with fixed class edges (20, 25 m/s); class means use the
-    GLOBAL unit count per slot (one all-reduce of the counts at setup).  The pool's validity is
-    computed once at ingest (its windows are resident for the whole run)."""
+    15-30 m/s, crossing at mid-window), i.e. each batch is `pool` new passes over the resident window
+    contents; a pass becomes one unit per pivot it crosses inside its window.  Slots = speed class x
+    pivot with fixed class edges (20, 25 m/s); class means use the GLOBAL unit count per slot (one
+    all-reduce of the counts at setup).  The batches merge into launches of `merge` batches, and every
+    launch validates the windows of all its passes (UnitScan: window per (batch, pass), 134 MB each, read
+    once per pass however many pivots it is imaged at): the reference divides a pass's window by
+    ||data||_F in every VirtualShotGather call (apis/virtual_shot_gather.py:125)."""
     from das_diff_veh_amd.plan import UnitPlan, sliding_pivots
-    from das_diff_veh_amd.vsg import flat_units, unit_sumsq
+    from das_diff_veh_amd.vsg import UnitScan, flat_units
     job = Job()
     n_ch, n_t, pool = wl["n_ch"], wl["n_t"], wl["pool"]
     t0 = time.time()
@@ -348,8 +352,7 @@ def build_sliding(wl, device, world, rank, scaling, chunk):
     n_total = wl["n_total"] if scaling == "weak" else -(-wl["n_total"] // world)
     rng = np.random.default_rng(1000 * rank + 7)
     n_batch = -(-int(n_total) // pool)
-    sumsq = window_sumsq(job.windows)
-    plans, slot_l = [], []
+    plans, slot_l, trks = [], [], []
     for _ in range(n_batch):
         x0 = rng.uniform(x_axis[edge], x_axis[-edge], pool)
         v = rng.uniform(15.0, 30.0, pool)
@@ -360,6 +363,7 @@ def build_sliding(wl, device, world, rank, scaling, chunk):
             trk.append((xs, np.round((ta + (xs - xa) / va) / TRACK_DT) * TRACK_DT))
         plan = UnitPlan.sliding(x_axis, t_axis, trk, pch, wl["half_aperture"], prm)
         plans.append(plan)
+        trks.append(trk)
         slot_l.append(np.digitize(v[plan.unit_window], [20.0, 25.0]) * n_piv + plan.unit_pivot)
     n_slot = 3 * n_piv
     counts = np.bincount(np.concatenate(slot_l), minlength=n_slot)
@@ -373,20 +377,27 @@ def build_sliding(wl, device, world, rank, scaling, chunk):
     merge = max(1, int(wl.get("merge", 1)))
     job.batches = []
     for m0 in range(0, len(plans), merge):
-        plan = UnitPlan.concat(plans[m0:m0 + merge]) if merge > 1 else plans[m0]
+        grp = plans[m0:m0 + merge]
+        plan = UnitPlan.concat(grp) if len(grp) > 1 else grp[0]
         sl = np.concatenate(slot_l[m0:m0 + merge])
-        job.batches.append(Batch(plan, StackSchedule(sl, n_slot, chunk=chunk, counts=counts),
-                                 flat_units(job.windows, plan), unit_sumsq(sumsq, plan),
-                                 torch.empty((plan.n_pass, 2), dtype=torch.float32, device=device),
-                                 derive=False, validity=False))
+        b = Batch(plan, StackSchedule(sl, n_slot, chunk=chunk, counts=counts), flat_units(job.windows, plan), None,
+                  torch.empty((plan.n_pass, 2), dtype=torch.float32, device=device), derive=False, validity=True)
+        b.scan = UnitScan(np.tile(np.arange(pool) * n_ch, len(grp)),
+                          np.concatenate([p.unit_window + k * pool for k, p in enumerate(grp)]), n_ch)
+        b.scan_bytes = 4 * b.scan.n_win * n_ch * n_t
+        job.batches.append(b)
     job.units = sum(p.n_pass for p in plans)
     job.n_local = n_batch * pool
     job.n_global = job.n_local * world
     job.t_plan = time.time() - t0
     job.cpu_sets = None
+    job.cpu_units = dict(x_axis=x_axis, t_axis=t_axis, pch=pch, trk=trks[0], plan=plans[0],
+                         half=wl["half_aperture"], units_per_pass=job.units / job.n_local)
     R, w = plans[0].R, plans[0].w
     pv, st, en, _ = sliding_pivots(x_axis, pch[:1], wl["half_aperture"])
     job.finish(n_slot, R, w, x_axis[st[0]:en[0]] - x_axis[pv[0]], t_axis[1] - t_axis[0], device)
+    job.work = torch.empty(max(max(b.plan.n_pass, b.scan.n_win) for b in job.batches) + 1, dtype=torch.int32,
+                           device=device)
     return job
 
 
@@ -407,7 +418,8 @@ def step(job, world, ev=None, fused=True):
         if ev is not None:
             ev[name][j][k].record()
     side = getattr(job, "side_streams", None)
-    if side and fused and all(b.validity and (b.plan.flags & 6) and not b.derive for b in job.batches):
+    if side and fused and getattr(job, "plan_all", None) is not None and \
+            all(b.validity and (b.plan.flags & 6) and not b.derive for b in job.batches):
         # every batch's tables in one launch, then every batch's scales (one wave per pass, latency bound)
         # spread over the main and side streams so they run side by side, then the stack launches
         main = torch.cuda.current_stream()
@@ -453,7 +465,8 @@ def step(job, world, ev=None, fused=True):
         mark("scales", j, 1)
         mark("stack", j, 0)
         if fuse:
-            vsg_stack_validated(b.win, b.plan, b.sched, scales=b.scales, out=job.stack, accumulate=j > 0, work=job.work)
+            vsg_stack_validated(b.win, b.plan, b.sched, scales=b.scales, out=job.stack, accumulate=j > 0, work=job.work,
+                                scan=getattr(b, "scan", None))
         else:
             vsg_stack(b.win, b.plan, b.sched, scales=b.scales, out=job.stack, accumulate=j > 0)
         mark("stack", j, 1)
@@ -535,6 +548,74 @@ def cpu_baseline(job, budget_s=20.0, workers=None):
                        f"saved windows, {sum(n for n, _ in res)} windows (VSG two-sided), f-v images at the 1-core "
                        f"cost / {workers}; 1 core: {n_win} windows ({per_window * 1e3:.1f} ms/window), {n_img} f-v "
                        f"images ({per_image * 1e3:.1f} ms/image) -> {rate1:.2f} windows/s; "
+                       f"cpu={platform.processor() or platform.machine()}",
+                value_1core=rate1)
+
+
+def cpu_baseline_sliding(job, budget_s=20.0, workers=None):
+    """configs[3] CPU path: oracle/ref_loop.gather (the reference's VirtualShotGather loop, including its
+    data / ||data||_F of the whole 4,096 x 8,192 window per call) for sample units of the bench's first
+    batch, each at its own pivot (start_x / end_x = pivot -/+ 200 m), on host copies of their windows.
+    1 core over the sample for budget_s / 2, then `workers` single-threaded processes for budget_s / 2;
+    passes/s = units/s / (units per pass), with the f-v images at the 1-core cost / workers."""
+    import tempfile
+    from oracle import ref_loop
+    torch.set_num_threads(1)
+    workers = workers or max(1, min(16, os.cpu_count() or 1))
+    cu = job.cpu_units
+    x_axis, t_axis, pch, trk, plan, half = (cu[k] for k in ("x_axis", "t_axis", "pch", "trk", "plan", "half"))
+    ns = min(4, plan.n_pass)
+    units = list(range(ns))
+    hosts = {}
+    for u in units:
+        q = int(plan.unit_window[u])
+        if q not in hosts:
+            hosts[q] = job.windows[q].to("cpu", torch.float64).numpy()
+    t_start, n_u, t_u, acc, ax = time.time(), 0, 0.0, None, None
+    while time.time() - t_start < budget_s / 2:
+        u = units[n_u % ns]
+        q, p = int(plan.unit_window[u]), float(x_axis[pch[int(plan.unit_pivot[u])]])
+        t0 = time.time()
+        g, gx, gt = ref_loop.gather(hosts[q], x_axis, t_axis, trk[q][0], trk[q][1], p, p - half, p + half)
+        t_u += time.time() - t0
+        n_u += 1
+        acc, ax = g, (gx, gt)
+    t0 = time.time()
+    ref_loop.disp_image(acc, *ax)
+    per_image = time.time() - t0
+    per_unit = t_u / n_u
+    upp = cu["units_per_pass"]
+    n_img = job.stack.shape[0]
+    rate1 = job.n_global / (per_unit * upp * job.n_global + per_image * n_img)
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    res = []
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "sample.npz")
+        qs = [int(plan.unit_window[u]) for u in units]
+        pv = np.array([float(x_axis[pch[int(plan.unit_pivot[u])]]) for u in units])
+        np.savez(path, wins=np.stack([hosts[q].astype(np.float32) for q in qs[:2]]), x_axis=x_axis, t_axis=t_axis,
+                 vx=np.stack([trk[q][0] for q in qs[:2]]), vt=np.stack([trk[q][1] for q in qs[:2]]), pivot=pv[:2],
+                 start_x=pv[:2] - half, end_x=pv[:2] + half)
+        procs = [subprocess.Popen([sys.executable, "-m", "oracle.ref_loop", path, str(wk), str(budget_s / 2)],
+                                  cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+                 for wk in range(workers)]
+        for pr in procs:
+            try:
+                out, _ = pr.communicate(timeout=budget_s * 6 + 120)
+                done, secs = out.split()
+                res.append((int(done), float(secs)))
+            except Exception:  # a worker that failed or hung does not count
+                pr.kill()
+    if not res:
+        raise RuntimeError("no CPU-baseline worker finished")
+    unit_rate = sum(n / t for n, t in res)
+    step_s = job.n_global * upp / unit_rate + per_image * n_img / len(res)
+    return dict(value=job.n_global / step_s, unit="vehicle-pass windows/s", cores=len(res), kind="port",
+                sample=f"all cores: {len(res)} single-threaded processes x {budget_s / 2:.0f} s, "
+                       f"{sum(n for n, _ in res)} (pass, pivot) units of 2 saved 4,096 x 8,192 windows (VSG two-sided, "
+                       f"+-{half:.0f} m at each unit's pivot); {upp:.2f} units per pass; f-v images at the 1-core cost / "
+                       f"{len(res)}; 1 core: {n_u} units ({per_unit * 1e3:.0f} ms/unit, the window's data / ||data|| "
+                       f"included), f-v image {per_image * 1e3:.1f} ms -> {rate1:.3f} passes/s; "
                        f"cpu={platform.processor() or platform.machine()}",
                 value_1core=rate1)
 
@@ -757,7 +838,8 @@ def measure(args, scaling, world, rank, device, cpu):
         if b.derive:
             b.plan.derive()
         corr_bytes.append(b.plan.algorithmic_bytes(out_rows=job.stack.shape[0] * job.stack.shape[1]))
-        win_bytes.append(4 * b.win.shape[0] * b.win.shape[1] * b.win.shape[2] if b.validity else 0)
+        win_bytes.append(getattr(b, "scan_bytes", 4 * b.win.shape[0] * b.win.shape[1] * b.win.shape[2]) if b.validity
+                         else 0)
     # a validated launch must read every window sample once (the correlation slices are subsets of
     # the window): its algorithmic bytes are the windows plus the stack rows written
     bytes_stack = [wb + out_bytes if f else cb for f, wb, cb in zip(fused, win_bytes, corr_bytes)]
@@ -811,6 +893,7 @@ def measure(args, scaling, world, rank, device, cpu):
                    "w": job.batches[0].plan.w, "parallelism": f"dp{world} (passes sharded, all-reduce of class stacks)",
                    "chunk": args.chunk, "gather_units_per_step_this_rank": job.units, "stack_launches_per_step": nb},
         "images_per_s": images_per_step * args.steps / elapsed,
+        "gather_units_per_s": job.units * (job.n_global / job.n_local) * args.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "vsg_stackv_kernel" if all(fused) else "vsg_stackf_kernel",
@@ -835,8 +918,8 @@ def measure(args, scaling, world, rank, device, cpu):
                             "instr_per_launch": valu, "source": valu_src, "clock_assumed_ghz": 2.4,
                             "model": "wave64 VALU instruction = 2 cycles on a SIMD-32 (>= 2 waves per SIMD) at the "
                                      "2.4 GHz max clock"}
-    if cpu and job.cpu_sets:
-        cb = cpu_baseline(job, args.cpu_budget)
+    if cpu and (job.cpu_sets or getattr(job, "cpu_units", None)):
+        cb = cpu_baseline(job, args.cpu_budget) if job.cpu_sets else cpu_baseline_sliding(job, args.cpu_budget)
         res["cpu_baseline"] = cb
         res["speedup_vs_cpu"] = res["value"] / cb["value"]
     else:

@@ -26,9 +26,10 @@ SIGNATURES = {
                           _p, _p],
     "dvh_vsg_scales": [_p, _i64, _i64, _i32, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p],
     "dvh_vsg_gathers": [_p, _i64, _i64, _i32, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p],
-    "dvh_vsg_stack": [_p, _i64, _i64, _i32, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p],
+    "dvh_vsg_stack": [_p, _i64, _i64, _i32, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _i32, _p, _p, _p, _p],
+    "dvh_vsg_stack_workspace": [_i32, _i32],
     "dvh_vsg_stack_validated": [_p, _i64, _i64, _i32, _i32, _i32, _p, _p, _i32, _i32, _i32, _i32, _p, _p, _p, _i32,
-                                _i32, _p, _p, _p, _p],
+                                _i32, _p, _p, _p, _i32, _p, _p, _p, _p],
     "dvh_disp_row_l1": [_p, _i64, _i64, _i32, _i32, _i32, _p, _p],
     "dvh_disp_tdft": [_p, _i64, _i64, _i32, _i32, _i32, _p, _i32, _p, _p, _p],
     "dvh_disp_fk": [_p, _i32, _i32, _i32, _p, _i32, _i32, _i32, _p, _p, _p, _i32, _p],
@@ -44,7 +45,7 @@ SIGNATURES = {
     "dvh_mute_traj": [_p, _i32, _i32, _i64, _i32, _i32, _p, _p, _p],
     "dvh_mute_time": [_p, _i32, _i64, _i32, _p, _p],
 }
-_RESTYPES = {"dvh_last_error": C.c_char_p}
+_RESTYPES = {"dvh_last_error": C.c_char_p, "dvh_vsg_stack_workspace": C.c_int64}
 
 _lock = threading.Lock()
 _lib = None

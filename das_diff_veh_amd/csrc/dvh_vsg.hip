@@ -30,7 +30,10 @@
 #include <stdint.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "vsg_engines.h"
+#include "vsg_engine_q.h"
 #include "dvh_common.h"
 #include "dvh.h"
 
@@ -41,6 +44,7 @@ constexpr int kBlock = 512;  // sumsq kernel
 // EngF500 fits 4
 template <class E> struct Occ { static constexpr int v = 3; };
 template <> struct Occ<EngF500> { static constexpr int v = 4; };
+template <> struct Occ<EngQ500> { static constexpr int v = 3; };  // 4 KB + 4 x 12 KB LDS per block: 3 blocks per CU
 #ifndef DVH_STACKF_OCC
 #define DVH_STACKF_OCC 0
 #endif
@@ -49,6 +53,36 @@ template <> struct Occ<EngF500> { static constexpr int v = 4; };
 template <class E> struct OccF {
   static constexpr int v = DVH_STACKF_OCC ? DVH_STACKF_OCC : (E::kWaves == 4 && E::NFFT <= 500 ? 4 : Occ<E>::v);
 };
+template <> struct OccF<EngQ500> { static constexpr int v = Occ<EngQ500>::v; };
+
+// One row task's cross spectra: EngQ500 takes the launch arguments (its slices are addressed per pass).
+template <class E>
+__device__ __forceinline__ void engine_spectra(E& eng, const VsgArgs& A, const RowTask& t, const RowTask& tn,
+                                               bool has_next, float2 (&Cf)[E::NH], float2 (&Co)[E::NH]) {
+  eng.spectra(t, tn, has_next, A.w, A.hop, Cf, Co);
+}
+template <>
+__device__ __forceinline__ void engine_spectra<EngQ500>(EngQ500& eng, const VsgArgs& A, const RowTask& t,
+                                                        const RowTask& tn, bool has_next, float2 (&Cf)[EngQ500::NH],
+                                                        float2 (&Co)[EngQ500::NH]) {
+  eng.spectra_q(A, t, t.p, t.row0, eng.ptab, tn, has_next, Cf, Co);
+}
+
+// max |x| bit pattern over what the last spectra call loaded (engines that validate their slices)
+template <class E>
+__device__ __forceinline__ uint32_t engine_vmax(const E&) { return 0u; }
+template <>
+__device__ __forceinline__ uint32_t engine_vmax<EngQ500>(const EngQ500& e) { return e.vmax; }
+template <>
+__device__ __forceinline__ uint32_t engine_vmax<EngF500>(const EngF500& e) { return e.rmax; }
+
+// Engines that read per-pass tables besides the windows (EngQ500: the shared pivot spectra) get them here.
+template <class E>
+__device__ __forceinline__ void bind_engine(E&, const VsgArgs&, const float2*) {}
+template <>
+__device__ __forceinline__ void bind_engine<EngQ500>(EngQ500& e, const VsgArgs&, const float2* ptab) {
+  e.ptab = ptab;
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -293,7 +327,7 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stack_kernel(V
                                                             const int32_t* __restrict__ order,
                                                             const int32_t* __restrict__ chunk_tab, int32_t n_chunk,
                                                             const float* __restrict__ weight,
-                                                            float* __restrict__ stack) {
+                                                            float* __restrict__ stack, const float2* __restrict__) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
   const int lane = threadIdx.x & 63;
@@ -364,7 +398,7 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = uni(chunk_tab[3 * c]), e = uni(chunk_tab[3 * c + 1]), slot = uni(chunk_tab[3 * c + 2]);
     int np = -1, ni = 0;
-    if (t + stride < n_task) {
+    if (E::kNextTask && t + stride < n_task) {
       const int c2 = uni((int)((t + stride) / A.R));
       ni = uni((int)((t + stride) % A.R));
       const int b2 = uni(chunk_tab[3 * c2]);
@@ -374,20 +408,25 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
     float2 Gh[NH];
 #pragma unroll
     for (int m = 0; m < NH; ++m) Gh[m] = make_float2(0.f, 0.f);
-    RowTask task = b < e ? make_task(A, uni(order[b]), i) : RowTask{};
-    uint32_t vmine = 0;  // validated launch: lane k holds max |receiver| of the chunk's k-th pass
+    RowTask task = (E::kNextTask && b < e) ? make_task(A, uni(order[b]), i) : RowTask{};
+    uint32_t vmine = 0;  // validated launch, skipping scan: lane k holds max |x| of the chunk's k-th pass's slices
     for (int q = b; q < e; ++q) {
       const int p = uni(order[q]);
       RowTask tn = task;
-      const bool has_next = (q + 1 < e) || np >= 0;
-      if (q + 1 < e) tn = make_task(A, uni(order[q + 1]), i);
-      else if (np >= 0) tn = make_task(A, np, ni);
+      bool has_next = false;
+      if (E::kNextTask) {  // engines that prefetch the next task's first sub-window get it
+        has_next = (q + 1 < e) || np >= 0;
+        if (q + 1 < e) tn = make_task(A, uni(order[q + 1]), i);
+        else if (np >= 0) tn = make_task(A, np, ni);
+      } else {
+        task = make_task(A, p, i);
+      }
       float2 Cf[NH], Co[NH];
-      eng.spectra(task, tn, has_next, A.w, A.hop, Cf, Co);
-      if (vflag) {  // the receiver samples this task loaded are validated here, not re-read by the scan
-        const uint32_t m = uni((int)wave_max_u32(eng.rmax));
+      engine_spectra(eng, A, task, tn, has_next, Cf, Co);
+      if (vflag) {  // the receiver slices this task loaded are validated here; the scan skips them
+        const uint32_t m = uni((int)wave_max_u32(engine_vmax(eng)));
         if (q - b < 64) {
-          if (lane_ == q - b) vmine = m;
+          if (lane_ == q - b) vmine = max(vmine, m);
         } else if (lane_ == 0) {
           atomicMax(vflag + p, m);
         }
@@ -480,19 +519,80 @@ template <class E>
 __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
     VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
     const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
-    float* __restrict__ stack) {
+    float* __restrict__ stack, const float2* __restrict__ ptab) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
+  bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6;
   stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave,
                   (int64_t)gridDim.x * E::kWaves);
+}
+
+// Spectra of the pivot's shared-window slices of every pass (EngQ500's table): one wave per pass
+// transforms the pivot row's slices pairwise per side (forward q = 0, 1 | 2 and other q = 0, 1 | 2;
+// sides never share a transform) and writes P[f], f <= 250, with the slice's non-zero flag at bin 255.
+__global__ __launch_bounds__(256) void vsg_pivot_spectra_kernel(VsgArgs A, float2* __restrict__ ptab) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float2* tw = reinterpret_cast<float2*>(lds);
+  init_twiddles<500>(tw);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float2* bufA = reinterpret_cast<float2*>(lds + sizeof(float2) * 500 + (size_t)wave * sizeof(float2) * 1000);
+  float2* bufB = bufA + 500;
+  for (int p = blockIdx.x * 4 + wave; p < A.n_pass; p += gridDim.x * 4) {
+    const int row0 = uni(A.pass_tab[2 * p]), pivot = uni(A.pass_tab[2 * p + 1]);
+    const RowTask t = make_task(A, p, pivot - row0);  // the pivot row: both sides shared
+#pragma unroll 1
+    for (int side = 0; side < 2; ++side) {
+      const int nw = side == 0 ? t.nwin_f : t.nwin_o;
+      const int a = side == 0 ? t.a_f : t.a_o;
+#pragma unroll 1
+      for (int q0 = 0; q0 < 3; q0 += 2) {
+        const int q1 = q0 + 1;
+        const bool h0 = q0 < nw, h1 = q1 < 3 && q1 < nw;
+        float2* o0 = ptab + ((int64_t)p * 6 + side * 3 + q0) * kPtabBins;
+        float2* o1 = ptab + ((int64_t)p * 6 + side * 3 + (q1 < 3 ? q1 : q0)) * kPtabBins;
+        uint32_t nz0 = 0, nz1 = 0;
+        const float2* X = nullptr;
+        if (h0 || h1) {
+          for (int n = lane; n < 500; n += 64) {
+            const float x0 = h0 ? t.piv[a + q0 * A.hop + n] : 0.f;
+            const float x1 = h1 ? t.piv[a + q1 * A.hop + n] : 0.f;
+            nz0 |= nzbits(x0);
+            nz1 |= nzbits(x1);
+            bufA[n] = make_float2(x0, x1);
+          }
+          wave_sync();
+          X = FftPlan<500>::T::run(bufA, bufB, tw, lane);
+        }
+        const bool l0 = __ballot(nz0 != 0) != 0, l1 = __ballot(nz1 != 0) != 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int f = lane + 64 * j;
+          float2 p0 = make_float2(0.f, 0.f), p1 = p0;
+          if (X && f <= 250) {
+            const float2 za = X[f], zc = X[f == 0 ? 0 : 500 - f];
+            p0 = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y - zc.y));
+            p1 = make_float2(0.5f * (za.y + zc.y), -0.5f * (za.x - zc.x));
+          }
+          if (f == kPtabBins - 1) {
+            p0 = make_float2(l0 ? 1.f : 0.f, 0.f);
+            p1 = make_float2(l1 ? 1.f : 0.f, 0.f);
+          }
+          o0[f] = p0;
+          if (q1 < 3) o1[f] = p1;
+        }
+        wave_sync();
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
 // Window validity fused into the stack launch.  The reference divides every window by ||data||_F
 // (preprocessing_window, apis/virtual_shot_gather.py:125): a NaN or inf anywhere in the window, or
 // an all-zero window, makes the whole gather NaN (norm / norm_amp divide by a NaN or zero maximum
-// afterwards), and so its class mean.  Deciding that needs every sample of the window, 4x - 30x the
+// afterwards), and so its class mean.  Deciding that needs every sample of the window, 4x - 130x the
 // bytes the correlations read.  In the validated stack launch, besides the correlation waves, one
 // wave per block streams the windows (16 x 16-byte loads per lane in flight) and keeps the maximum
 // of |x| as a bit pattern, max(bits & 0x7fffffff): >= 0x7f800000 means a NaN / inf, 0 means all
@@ -500,24 +600,17 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
 // from the start and by the correlation waves once their row tasks are done, so the HBM-bound scan
 // runs under the VALU-bound transforms.  vsg_invalid_fill_kernel then sets the class slots holding an
 // invalid pass to NaN.
+//
+// Scan windows: by default window s is pass s (win + s * pass_stride, n_ch rows), scanned in the
+// correlation's class-sorted order so that both fronts start on the same passes (3.51 vs 3.53 ms per
+// synth10k launch).  A unit launch (plan.UnitPlan: (pass, pivot) units over one flattened record) names
+// its windows instead: scan_tab[s] = first record row of window s, and unit_scan[u] = the window whose
+// flag unit u takes, so a pass imaged at several pivots is validated once per launch.
 constexpr int kScanRows = 16;
-#ifndef DVH_SCAN_DEPTH
-#define DVH_SCAN_DEPTH 16
-#endif
-constexpr int kScanDepth = DVH_SCAN_DEPTH;
-#ifndef DVH_SCAN_AUX
-#define DVH_SCAN_AUX 2  // cache policy of the scan's buffer loads (2 = nt, 16 = sc1: both bypass L1)
-#endif
-#ifndef DVH_SCAN_COMPLEMENT
-#define DVH_SCAN_COMPLEMENT 0  // skip the blocks the correlation waves validate
-#endif
-#ifndef DVH_SCAN_ORDER
-#define DVH_SCAN_ORDER 1  // scan the passes in the correlation's (class-sorted) order, not index order: 3.51 vs
-                          // 3.53 ms per synth10k launch (tools/gpu_r2aj.sh; allocating loads, AUX 0, lost 4 %)
-#endif
+constexpr int kScanDepth = 16;
+constexpr int kScanAux = 2;  // cache policy of the scan's buffer loads (nt; allocating loads measured 4 % slower)
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
-
 
 __device__ __forceinline__ int pull_unit(uint32_t* counter, int lane) {
   int u = 0;
@@ -547,7 +640,7 @@ __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int n
   u32x4 r[kScanDepth];
 #pragma unroll
   for (int d = 0; d < kScanDepth; ++d) {
-    r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, DVH_SCAN_AUX);
+    r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kScanAux);
     off += 1024;
   }
   for (int s0 = 0; s0 < nsteps; s0 += kScanDepth) {
@@ -555,77 +648,18 @@ __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int n
     for (int d = 0; d < kScanDepth; ++d) {
       const u32x4 v = r[d] & 0x7fffffffu;
       m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
-      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, DVH_SCAN_AUX);
+      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kScanAux);
       off += 1024;
     }
   }
   return m;
 }
 
-// LDS-DMA scan: 1 KiB pieces (one global_load_lds_dwordx4 per wave) land in a ring of RING pieces of this
-// wave's LDS without passing through VGPRs, so a scan wave keeps RING KiB in flight beside its register
-// loads at no register cost.  Written with the M0 recipe of cdna_hip_programming.md (the compiler does
-// not count these loads: the waits below are explicit).
-#ifndef DVH_CORR_PRIO
-#define DVH_CORR_PRIO 2  // s_setprio of the correlation waves while they correlate (scan waves stay at 0): the
-                         // correlation is the critical path; 1 / 2 / 3 all measured 127.7 k -> 136 k windows/s on synth10k
-#endif
-#ifndef DVH_SCAN_RING
-#define DVH_SCAN_RING 0  // KiB of LDS ring per dedicated scan wave (0: register loads only; 8 / 16 measured
-                         // 12-17 % slower on synth10k: the faster scan lengthens the correlation waves' load latency)
-#endif
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-  unsigned keep;
-  // lgkmcnt(0) first: the wave's read of the slot this piece overwrites has returned
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-
-// max |x| bit pattern over nf4 consecutive float4 (16-byte aligned) through the LDS ring `ring`
-// (RING KiB, wave-private).  Lanes past the end re-read the last float4: a duplicate leaves the max as is.
-typedef __attribute__((address_space(3))) char lds_char;
-template <int RING>
-__device__ __forceinline__ uint32_t scan_span_ring(const float* __restrict__ q, int nf4, int lane, char* ring_) {
-  const int np = (nf4 + 63) >> 6;
-  // the ring as an LDS (address space 3) pointer: ds_read for the pieces (a flat read would count on vmcnt
-  // and its wait would drain the ring) and the LDS byte offset M0 takes
-  lds_char* ring = (lds_char*)ring_;
-  const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(ring));
-  auto issue = [&](int piece, int slot) {
-    const int i = min(piece * 64 + lane, nf4 - 1);
-    glds16(q + 4 * (int64_t)i, base + (uint32_t)slot * 1024u);
-  };
-  const int pre = np < RING ? np : RING;
-  for (int k = 0; k < pre; ++k) issue(k, k);
-  uint32_t m = 0;
-  int slot = 0;
-  for (int k = 0; k < np; ++k) {
-    if (np - k >= RING) wait_vm<RING - 1>();  // piece k has landed (RING - 1 younger ones in flight)
-    else wait_vm<0>();
-    const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(ring + slot * 1024 + lane * 16) &
-                    0x7fffffffu;
-    m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
-    if (k + RING < np) issue(k + RING, slot);
-    slot = slot + 1 == RING ? 0 : slot + 1;
-  }
-  return m;
-}
-
-// rows [c0, c1) of a window (n_t samples each): max |x| bit pattern over the wave; ring (nullable):
-// this wave's LDS-DMA ring of `ring_kib` pieces (16 or 8 KiB)
+// rows [c0, c1) of a window (n_t samples each): max |x| bit pattern over the wave
 __device__ __forceinline__ uint32_t scan_rows(const float* __restrict__ base, int64_t ch_stride, int c0, int c1,
-                                              int n_t, bool vec, int lane, char* ring = nullptr, int ring_kib = 0) {
+                                              int n_t, bool vec, int lane) {
   uint32_t m = 0;
-  if (vec && ch_stride == n_t && ring) {  // contiguous rows through the LDS ring
-    const float* q = base + (int64_t)c0 * ch_stride;
-    const int nf4 = ((c1 - c0) * n_t) >> 2;
-    m = ring_kib >= 16 ? scan_span_ring<16>(q, nf4, lane, ring) : scan_span_ring<8>(q, nf4, lane, ring);
-  } else if (vec && ch_stride == n_t) {  // the unit's rows are one contiguous span
+  if (vec && ch_stride == n_t) {  // the unit's rows are one contiguous span
     m = scan_span(base + (int64_t)c0 * ch_stride, ((c1 - c0) * n_t) >> 2, lane);
   } else if (vec) {
     for (int c = c0; c < c1; ++c) m = max(m, scan_span(base + (int64_t)c * ch_stride, n_t >> 2, lane));
@@ -636,166 +670,136 @@ __device__ __forceinline__ uint32_t scan_rows(const float* __restrict__ base, in
   return wave_max_u32(m);
 }
 
-// Blocks of kScanBlk samples: the scan reads whole blocks, one wave-wide 16-byte load each.  The rows a
-// correlation wave loads from (its gather row's forward / other-side slices, as far as the sub-windows
-// reach) are validated by that wave (stackf_tasks), so the scan skips the blocks lying entirely inside
-// them and every window byte is fetched from HBM about once.
-constexpr int kScanBlk = 256;
-constexpr int kScanListBytes = kScanRows * 64 * 4;  // per scanning wave: <= 64 blocks per row
+struct ScanArgs {
+  const int32_t* tab;  // nullptr: window s = pass s; else first record row of window s
+  int32_t n_win;       // scan windows
+  int32_t n_ch, n_t;   // rows and samples of one window
+  int32_t skip;        // 1: skip the receiver slices the correlation waves validate (window s = pass s)
+};
 
-__device__ __forceinline__ uint64_t scan_mask(const VsgArgs& A, int p, int c, int n_t) {
-  const int nb = (n_t + kScanBlk - 1) / kScanBlk;
-  const uint64_t all = nb >= 64 ? ~0ull : ((1ull << nb) - 1);
-  const int i = c - A.pass_tab[2 * p];
-  if (i < 0 || i >= A.R) return all;
+// The sample range [lo, hi) of row c of pass p that the correlation waves load (the row's receiver
+// slices: each side's sub-windows [a, a + (nwin - 1) hop + w)), shrunk to whole float4; both empty
+// outside the gather and on the pivot row (whose shared slices the table kernel reads, unvalidated).
+__device__ __forceinline__ void skip_ranges(const VsgArgs& A, int p, int c, int& lo1, int& hi1, int& lo2, int& hi2) {
+  lo1 = hi1 = lo2 = hi2 = 0;
+  const int row0 = uni(A.pass_tab[2 * p]), pivot = uni(A.pass_tab[2 * p + 1]);
+  const int i = c - row0;
+  if (i < 0 || i >= A.R || c == pivot) return;
   const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
-  int lo[2] = {0, 0}, hi[2] = {0, 0};
-  const int sides = (A.flags & kFlagOtherSide) ? 2 : 1;
-  for (int sd = 0; sd < sides; ++sd) {
-    const int nw = n_subwin(seg[2 * sd + 1], A.w, A.hop);
-    lo[sd] = seg[2 * sd];
-    hi[sd] = nw > 0 ? lo[sd] + (nw - 1) * A.hop + A.w : lo[sd];
+  const int nf = n_subwin(uni(seg[1]), A.w, A.hop);
+  if (nf > 0) {
+    const int a = uni(seg[0]);
+    lo1 = (a + 3) & ~3;
+    hi1 = (a + (nf - 1) * A.hop + A.w) & ~3;
   }
-  if (hi[0] > lo[0] && hi[1] > lo[1] && lo[1] <= hi[0] && lo[0] <= hi[1]) {  // overlapping: one interval
-    lo[0] = min(lo[0], lo[1]);
-    hi[0] = max(hi[0], hi[1]);
-    hi[1] = lo[1];
+  const int no = (A.flags & kFlagOtherSide) ? n_subwin(uni(seg[3]), A.w, A.hop) : 0;
+  if (no > 0) {
+    const int a = uni(seg[2]);
+    lo2 = (a + 3) & ~3;
+    hi2 = (a + (no - 1) * A.hop + A.w) & ~3;
   }
-  uint64_t m = all;
-  for (int sd = 0; sd < 2; ++sd) {
-    if (hi[sd] <= lo[sd]) continue;
-    const int b0 = (lo[sd] + kScanBlk - 1) / kScanBlk;                 // first block starting inside
-    const int b1 = hi[sd] >= n_t ? nb : hi[sd] / kScanBlk;             // blocks ending inside
-    for (int b = b0; b < b1; ++b) m &= ~(1ull << b);
-  }
-  return m;
 }
 
-// rows [c0, c1) (<= 64) of window p, rows contiguous (ch_stride == n_t): the rows' block offsets are
-// listed in LDS, then streamed with kScanDepth loads per lane in flight across rows
-__device__ __forceinline__ uint32_t scan_unit_blocks(const VsgArgs& A, int p, int c0, int c1, int n_ch, int n_t,
-                                                     uint32_t* __restrict__ list, int lane) {
-  const int nr = c1 - c0;
-  uint64_t mask = 0;
-  int cnt = 0;
-  if (lane < nr) {
-    mask = scan_mask(A, p, c0 + lane, n_t);
-    cnt = __popcll(mask);
-  }
-  int pre = cnt;  // inclusive prefix over lanes
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(pre, o);
-    if (lane >= o) pre += t;
-  }
-  const int total = __builtin_amdgcn_readfirstlane(__shfl(pre, 63));
-  if (lane < nr) {
-    int k = pre - cnt;
-    const uint32_t row = (uint32_t)(c0 + lane) * (uint32_t)n_t;
-    while (mask) {
-      const int b = __ffsll((long long)mask) - 1;
-      mask &= mask - 1;
-      list[k++] = row + (uint32_t)(b * kScanBlk);
-    }
-  }
-  wave_sync();
-  const uint32_t wbytes = (uint32_t)n_ch * (uint32_t)n_t * 4u;
-  const __amdgpu_buffer_rsrc_t rs = scan_rsrc(A.win + (int64_t)p * A.pass_stride, wbytes);
-  const uint32_t oob = (uint32_t)n_ch * (uint32_t)n_t;  // a block offset past the window: loads return 0
+// scan_span over the contiguous rows [c0, c1) of pass p's window, with the loads of each row's receiver
+// slices replaced by out-of-range offsets (no memory request, zero): those samples were validated by the
+// correlation waves.  n_t is a multiple of 16 KB / 4 (16 wave loads of 1 KB), so every batch of kScanDepth
+// loads lies in one row; each row's ranges are fetched one row ahead.
+__device__ __forceinline__ uint32_t scan_rows_skip(const VsgArgs& A, int p, const float* __restrict__ base, int c0,
+                                                   int c1, int n_t, int lane) {
+  const int cpr = n_t >> 8;  // 1 KB chunks per row (a multiple of kScanDepth)
+  const int nch = (c1 - c0) * cpr;
+  const __amdgpu_buffer_rsrc_t rs = scan_rsrc(base + (int64_t)c0 * n_t, (uint32_t)((c1 - c0) * n_t) * 4u);
+  int cur[4], nxt[4];
+  skip_ranges(A, p, c0, cur[0], cur[1], cur[2], cur[3]);
+  skip_ranges(A, p, c0 + 1 < c1 ? c0 + 1 : c0, nxt[0], nxt[1], nxt[2], nxt[3]);
+  int row = 0;
+  auto off = [&](int ch, const int (&g)[4]) -> int {
+    const int col = (ch - row * cpr) * 256 + lane * 4;
+    const bool sk = (col >= g[0] && col + 4 <= g[1]) || (col >= g[2] && col + 4 <= g[3]);
+    return sk ? 0x7ffffff0 : ch * 1024 + lane * 16;
+  };
   uint32_t m = 0;
   u32x4 r[kScanDepth];
 #pragma unroll
-  for (int d = 0; d < kScanDepth; ++d) {
-    const uint32_t off = d < total ? list[d] : oob;
-    r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((off + 4u * lane) * 4u), 0, DVH_SCAN_AUX);
-  }
-  for (int s0 = 0; s0 < total; s0 += kScanDepth) {
+  for (int d = 0; d < kScanDepth; ++d) r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off(d, cur), 0, kScanAux);
+  for (int s0 = 0; s0 < nch; s0 += kScanDepth) {
+    const int c = s0 + kScanDepth;  // first chunk this batch issues
+    const bool more = c < nch;
+    if (more && c == (row + 1) * cpr) {  // the batch starts a new row: its ranges were fetched a row ago
+      ++row;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+      const int rn = c0 + row + 1 < c1 ? c0 + row + 1 : c0 + row;
+      skip_ranges(A, p, rn, nxt[0], nxt[1], nxt[2], nxt[3]);
+    }
 #pragma unroll
     for (int d = 0; d < kScanDepth; ++d) {
       const u32x4 v = r[d] & 0x7fffffffu;
       m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
-      const int sn = s0 + d + kScanDepth;
-      const uint32_t off = sn < total ? list[sn] : oob;
-      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((off + 4u * lane) * 4u), 0, DVH_SCAN_AUX);
+      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, more ? off(c + d, cur) : 0x7ffffff0, 0, kScanAux);
     }
   }
-  wave_sync();  // the list is rewritten by the next unit
   return wave_max_u32(m);
 }
 
-// Pull scan units (pass, kScanRows channel rows) until none is left; atomicMax into vflag[pass].
-// list: this wave's LDS scratch of kScanListBytes.
-__device__ __forceinline__ void scan_units(const VsgArgs& A, int n_ch, int n_t, uint32_t* __restrict__ vflag,
-                                           uint32_t* __restrict__ counter, uint32_t* __restrict__ list, int lane,
-                                           char* ring = nullptr, int ring_kib = 0,
+// Pull scan units (window, kScanRows channel rows) until none is left; atomicMax into vflag[window].
+__device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, uint32_t* __restrict__ vflag,
+                                           uint32_t* __restrict__ counter, int lane,
                                            const int32_t* __restrict__ sorder = nullptr) {
-  const int upp = (n_ch + kScanRows - 1) / kScanRows;  // units per pass
-  const int n_units = A.n_pass * upp;
-  const bool vec = (n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
+  const int upp = (S.n_ch + kScanRows - 1) / kScanRows;  // units per window
+  const int n_units = S.n_win * upp;
+  const bool vec = (S.n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
                    (reinterpret_cast<uintptr_t>(A.win) % 16 == 0);
-  // complement blocks: contiguous rows, <= 64 blocks per row, a window under 4 GiB
-  const bool blocks = DVH_SCAN_COMPLEMENT && vec && A.ch_stride == n_t && n_t >= kScanBlk && n_t <= 64 * kScanBlk &&
-                      (int64_t)n_ch * n_t * 4 < (1ll << 32) && list != nullptr;
+  const bool skip = S.skip && !S.tab && vec && A.ch_stride == S.n_t && S.n_t % (256 * kScanDepth) == 0 &&
+                    (int64_t)S.n_ch * S.n_t < (1ll << 29);
   int u = pull_unit(counter, lane);
   while (u < n_units) {
     const int un = pull_unit(counter, lane);  // the next unit's index, fetched under this unit's loads
     const int q = u / upp, c0 = (u - q * upp) * kScanRows;
-    const int p = sorder ? uni(sorder[q]) : q;
-    const int c1 = min(c0 + kScanRows, n_ch);
-    const uint32_t m = blocks ? scan_unit_blocks(A, p, c0, c1, n_ch, n_t, list, lane)
-                              : scan_rows(A.win + (int64_t)p * A.pass_stride, A.ch_stride, c0, c1, n_t, vec, lane,
-                                          ring, ring_kib);
-    if (lane == 0) atomicMax(vflag + p, m);
+    const int s = (sorder && !S.tab) ? uni(sorder[q]) : q;
+    const float* base = S.tab ? A.win + (int64_t)uni(S.tab[s]) * A.ch_stride : A.win + (int64_t)s * A.pass_stride;
+    const uint32_t m = skip ? scan_rows_skip(A, s, base, c0, min(c0 + kScanRows, S.n_ch), S.n_t, lane)
+                            : scan_rows(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
+    if (lane == 0) atomicMax(vflag + s, m);
     u = un;
   }
 }
 
+#ifndef DVH_CORR_PRIO
+#define DVH_CORR_PRIO 2  // s_setprio of the correlation waves while they correlate (scan waves stay at 0): the
+                         // correlation is the critical path; 1 / 2 / 3 all measured 127.7 k -> 136 k windows/s on synth10k
+#endif
+
 // Persistent validated stack launch: blocks of kFft correlation waves + kScan scan waves, two per CU.
-template <class E, int kFft, int kScan>
-__global__ __launch_bounds__(64 * (kFft + kScan), 4) void vsg_stackv_kernel(
+template <class E, int kFft, int kScan, int kOcc>
+__global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
     const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
-    float* __restrict__ stack, int32_t n_ch, int32_t n_t, uint32_t* __restrict__ vflag, uint32_t* __restrict__ counter) {
+    float* __restrict__ stack, ScanArgs S, uint32_t* __restrict__ vflag, uint32_t* __restrict__ counter,
+    const float2* __restrict__ ptab) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
+  bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t* list;
-  char* ring = nullptr;
-  int ring_kib = 0;
-#if DVH_CORR_PRIO
-  if (wave < kFft) __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
-#endif
   if (wave < kFft) {
+#if DVH_CORR_PRIO
+    __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
+#endif
     stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
-                    (int64_t)gridDim.x * kFft, DVH_SCAN_COMPLEMENT ? vflag : nullptr);
-    list = reinterpret_cast<uint32_t*>(lds + E::kBlockBytes + (size_t)wave * E::kWaveBytes);  // its FFT buffers
+                    (int64_t)gridDim.x * kFft, S.skip ? vflag : nullptr);
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
-    if (DVH_SCAN_RING && !DVH_SCAN_COMPLEMENT && E::kWaveBytes >= 8192) {  // done correlating: its buffers
-      ring = lds + E::kBlockBytes + (size_t)wave * E::kWaveBytes;
-      ring_kib = 8;
-    }
-  } else {
-    list = reinterpret_cast<uint32_t*>(lds + E::kBlockBytes + (size_t)kFft * E::kWaveBytes +
-                                       (size_t)(wave - kFft) * kScanListBytes);
-    if (DVH_SCAN_RING && !DVH_SCAN_COMPLEMENT) {
-      ring = lds + E::kBlockBytes + (size_t)kFft * E::kWaveBytes + (size_t)(wave - kFft) * DVH_SCAN_RING * 1024;
-      ring_kib = DVH_SCAN_RING;
-    }
   }
-  const int32_t* sorder = nullptr;
-#if DVH_SCAN_ORDER
   // the chunks cover order[0, end of the last chunk): scan in that order when it lists every pass
-  if (n_chunk > 0 && uni(chunk_tab[3 * (n_chunk - 1) + 1]) == A.n_pass) sorder = order;
-#endif
-  scan_units(A, n_ch, n_t, vflag, counter, DVH_SCAN_COMPLEMENT ? list : nullptr, lane, ring, ring_kib, sorder);
+  const int32_t* sorder = (n_chunk > 0 && uni(chunk_tab[3 * (n_chunk - 1) + 1]) == A.n_pass) ? order : nullptr;
+  scan_units(A, S, vflag, counter, lane, sorder);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
-__global__ __launch_bounds__(256) void window_scan_kernel(VsgArgs A, int32_t n_ch, int32_t n_t,
-                                                          uint32_t* __restrict__ vflag, uint32_t* __restrict__ counter) {
-  scan_units(A, n_ch, n_t, vflag, counter, nullptr, threadIdx.x & 63);  // no correlation waves: whole rows
+__global__ __launch_bounds__(256) void window_scan_kernel(VsgArgs A, ScanArgs S, uint32_t* __restrict__ vflag,
+                                                          uint32_t* __restrict__ counter) {
+  scan_units(A, S, vflag, counter, threadIdx.x & 63);
 }
 
 // stack[slot] = NaN for every slot holding a pass whose window is invalid (vflag NaN / inf or 0).
@@ -805,13 +809,15 @@ constexpr int kFillBlock = 256;
 __global__ __launch_bounds__(kFillBlock) void vsg_invalid_fill_kernel(const int32_t* __restrict__ order,
                                                                       const int32_t* __restrict__ chunk_tab,
                                                                       int32_t n_chunk, const uint32_t* __restrict__ vflag,
+                                                                      const int32_t* __restrict__ unit_scan,
                                                                       float* __restrict__ stack, int64_t slot_elems) {
   const int slot = blockIdx.y;
   int bad = 0;
   for (int c = threadIdx.x; c < n_chunk; c += kFillBlock) {
     if (chunk_tab[3 * c + 2] != slot) continue;
     for (int q = chunk_tab[3 * c]; q < chunk_tab[3 * c + 1]; ++q) {
-      const uint32_t f = vflag[order[q]];
+      const int p = order[q];
+      const uint32_t f = vflag[unit_scan ? unit_scan[p] : p];
       bad |= (f >= 0x7f800000u) || (f == 0u);
     }
   }
@@ -997,54 +1003,92 @@ static int cu_count() {
 }
 
 #ifndef DVH_VSTACK_FFT
-#define DVH_VSTACK_FFT 7  // correlation waves per block of the validated stack launch
+#define DVH_VSTACK_FFT 7  // EngF500: correlation waves per block of the validated stack launch (2 blocks per CU)
 #endif
 #ifndef DVH_VSTACK_SCAN
 #define DVH_VSTACK_SCAN 1  // scan waves per block
 #endif
+#ifndef DVH_SCAN_SKIP
+#define DVH_SCAN_SKIP 0  // 1: the validated launch's scan skips the receiver slices the correlation validates
+#endif
+#ifndef DVH_QSTACK_FFT
+#define DVH_QSTACK_FFT 5  // EngQ500: correlation waves per validated block (12 KB of LDS each), 2 blocks per CU
+#endif
+#ifndef DVH_QSTACK_SCAN
+#define DVH_QSTACK_SCAN 1
+#endif
+
+// EngQ500 (the four-step engine with the per-pass pivot spectra table) takes w = N = 500 when the
+// caller gives the table's workspace and a pass's gather rows are addressable by 31-bit byte offsets
+static bool use_q(int n, const VsgArgs& A, const void* ws) {
+  return n == 500 && ws != nullptr && (int64_t)A.R * A.ch_stride * 4 < (1ll << 31) && A.ch_stride >= 0;
+}
+
+static int launch_ptab(VsgArgs& A, float2* ptab, hipStream_t s) {
+  const int grid = (int)std::min<int64_t>(((int64_t)A.n_pass + 3) / 4, 8 * (int64_t)cu_count());
+  void* args[] = {&A, &ptab};
+  return launch((const void*)vsg_pivot_spectra_kernel, grid, 4, sizeof(float2) * (500 + 4 * 1000), args, s);
+}
+
+DVH_API int64_t dvh_vsg_stack_workspace(int32_t n_pass, int32_t w) {
+  bool pad;
+  return (choose_fft(w, &pad) == 500 && n_pass > 0) ? (int64_t)n_pass * kPtabPerPass * (int64_t)sizeof(float2) : 0;
+}
 
 DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass,
                                     int32_t n_ch, int32_t n_t, const int32_t* pass_tab, const int32_t* seg_tab, int32_t R,
                                     int32_t w, int32_t hop, int32_t flags, const float* scales, const int32_t* order,
                                     const int32_t* chunk_tab, int32_t n_chunk, int32_t n_slot, const float* weight,
-                                    float* stack, uint32_t* work, void* stream) {
+                                    float* stack, const int32_t* scan_tab, int32_t n_scan, const int32_t* unit_scan,
+                                    uint32_t* work, void* spec_ws, void* stream) {
   VsgArgs A{win, pass_stride, ch_stride, pass_tab, seg_tab, n_pass, R, w, hop, flags};
   if (int rc = check_common(A)) return rc;
   if (!scales || !order || !chunk_tab || !weight || !stack || !work) return set_error(-2, "null pointer argument");
   if (!(flags & (kFlagNorm | kFlagNormAmp)))
     return set_error(-2, "validated stacking needs norm or norm_amp (raw scales need ||data||_F: dvh_window_sumsq)");
   if (n_ch < R || n_t <= 0) return set_error(-2, "window smaller than the gather");
+  if ((scan_tab == nullptr) != (unit_scan == nullptr)) return set_error(-2, "scan_tab and unit_scan go together");
+  if (scan_tab && n_scan <= 0) return set_error(-2, "a scan table needs n_scan > 0");
   VsgKernels k;
   int n;
   if (!get_kernels(w, &k, &n)) return set_error(-4, "unsupported correlation window length");
+  ScanArgs S{scan_tab, scan_tab ? n_scan : n_pass, n_ch, n_t, 0};
   hipStream_t s = (hipStream_t)stream;
   uint32_t* vflag = work;
-  uint32_t* counter = work + n_pass;
-  hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t) * ((size_t)n_pass + 1), s);
+  uint32_t* counter = work + S.n_win;
+  float2* ptab = reinterpret_cast<float2*>(spec_ws);
+  hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t) * ((size_t)S.n_win + 1), s);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
   const int64_t tasks = (int64_t)n_chunk * R;
   if (n == 500 && DVH_FREQ_STACK) {
-    constexpr int F = DVH_VSTACK_FFT, S = DVH_VSTACK_SCAN;
-    const void* fn = (const void*)vsg_stackv_kernel<EngF500, F, S>;
-    static_assert(EngF500::kWaveBytes >= kScanListBytes, "a correlation wave's buffers hold its scan list");
-    static_assert(DVH_SCAN_RING == 0 || DVH_SCAN_RING == 8 || DVH_SCAN_RING == 16, "scan ring: 0, 8 or 16 KiB");
-    const size_t scan_lds = DVH_SCAN_COMPLEMENT ? kScanListBytes : (size_t)DVH_SCAN_RING * 1024;
-    const size_t lds = EngF500::kBlockBytes + F * EngF500::kWaveBytes + S * scan_lds;
+    const bool q = use_q(n, A, spec_ws);
+    if (q) {
+      if (int rc = launch_ptab(A, ptab, s)) return rc;
+      S.skip = DVH_SCAN_SKIP && !scan_tab;  // EngQ500 validates the receiver slices it loads
+    } else {
+      ptab = nullptr;
+      S.skip = DVH_SCAN_SKIP && !scan_tab;  // EngF500 validates the receiver slices it loads (rmax)
+    }
+    const int F = q ? DVH_QSTACK_FFT : DVH_VSTACK_FFT, SC = q ? DVH_QSTACK_SCAN : DVH_VSTACK_SCAN;
+    const void* fn = q ? (const void*)vsg_stackv_kernel<EngQ500, DVH_QSTACK_FFT, DVH_QSTACK_SCAN, 3>
+                       : (const void*)vsg_stackv_kernel<EngF500, DVH_VSTACK_FFT, DVH_VSTACK_SCAN, 4>;
+    const size_t lds = q ? EngQ500::kBlockBytes + F * EngQ500::kWaveBytes : EngF500::kBlockBytes + F * EngF500::kWaveBytes;
     const int64_t need = (tasks + F - 1) / F;
     const int grid = (int)(need < 2 * cu_count() ? (need > 0 ? need : 1) : 2 * cu_count());
-    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &n_ch, &n_t, &vflag, &counter};
-    if (int rc = launch(fn, grid, F + S, lds, args, s)) return rc;
+    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &ptab};
+    if (int rc = launch(fn, grid, F + SC, lds, args, s)) return rc;
   } else {  // other engines: the scan as its own launch, then the plain stack launch
-    void* sargs[] = {&A, &n_ch, &n_t, &vflag, &counter};
+    void* sargs[] = {&A, (void*)&S, &vflag, &counter};
     if (int rc = launch((const void*)window_scan_kernel, 4 * cu_count(), 4, 0, sargs, s)) return rc;
     const int64_t grid = (tasks + k.waves - 1) / k.waves;
-    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack};
+    ptab = nullptr;
+    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &ptab};
     if (int rc = launch(k.stack, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, s)) return rc;
   }
   if (n_slot <= 0 || n_chunk <= 0) return 0;
   const int64_t slot_elems = (int64_t)R * w;
   hipLaunchKernelGGL(vsg_invalid_fill_kernel, dim3((unsigned)((slot_elems + 4095) / 4096), n_slot), dim3(kFillBlock), 0,
-                     s, order, chunk_tab, n_chunk, (const uint32_t*)vflag, stack, slot_elems);
+                     s, order, chunk_tab, n_chunk, (const uint32_t*)vflag, unit_scan, stack, slot_elems);
   e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
 }
@@ -1052,7 +1096,7 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
 DVH_API int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass,
                           const int32_t* pass_tab, const int32_t* seg_tab, int32_t R, int32_t w, int32_t hop,
                           int32_t flags, const float* scales, const int32_t* order, const int32_t* chunk_tab,
-                          int32_t n_chunk, const float* weight, float* stack, void* stream) {
+                          int32_t n_chunk, const float* weight, float* stack, void* spec_ws, void* stream) {
   VsgArgs A{win, pass_stride, ch_stride, pass_tab, seg_tab, n_pass, R, w, hop, flags};
   if (int rc = check_common(A)) return rc;
   if (!scales || !order || !chunk_tab || !weight || !stack) return set_error(-2, "null pointer argument");
@@ -1060,7 +1104,19 @@ DVH_API int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stri
   int n;
   if (!get_kernels(w, &k, &n)) return set_error(-4, "unsupported correlation window length");
   const int64_t tasks = (int64_t)n_chunk * R;
-  const int64_t grid = (tasks + k.waves - 1) / k.waves;
-  void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack};
-  return launch(k.stack, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  float2* ptab = nullptr;
+  const void* fn = k.stack;
+  int waves = k.waves;
+  size_t lds = k.lds;
+  if (DVH_FREQ_STACK && use_q(n, A, spec_ws)) {
+    ptab = reinterpret_cast<float2*>(spec_ws);
+    if (int rc = launch_ptab(A, ptab, s)) return rc;
+    fn = (const void*)vsg_stackf_kernel<EngQ500>;
+    waves = EngQ500::kWaves;
+    lds = EngQ500::kBlockBytes + EngQ500::kWaves * EngQ500::kWaveBytes;
+  }
+  const int64_t grid = (tasks + waves - 1) / waves;
+  void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &ptab};
+  return launch(fn, (int)(grid > (1 << 30) ? (1 << 30) : grid), waves, lds, args, s);
 }

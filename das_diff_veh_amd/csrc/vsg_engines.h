@@ -85,6 +85,7 @@ struct RowTask {
   const float* rcv;
   int a_f, nwin_f, a_o, nwin_o;
   int ch, pivot;
+  int p, row0;
 };
 
 __device__ __forceinline__ RowTask make_task(const VsgArgs& A, int p, int i) {
@@ -92,6 +93,8 @@ __device__ __forceinline__ RowTask make_task(const VsgArgs& A, int p, int i) {
   i = uni(i);
   RowTask t;
   const int row0 = uni(A.pass_tab[2 * p]);
+  t.p = p;
+  t.row0 = row0;
   t.pivot = uni(A.pass_tab[2 * p + 1]);
   t.ch = row0 + i;
   const float* base = A.win + (int64_t)p * A.pass_stride;
@@ -138,6 +141,7 @@ template <int N, bool PAD>
 struct EngStockham {
   static constexpr int NFFT = N;
   static constexpr int kWaves = 4;
+  static constexpr bool kNextTask = false;
   static constexpr int NJ = (N + 63) / 64;
   static constexpr int NH = (N / 2 + 1 + 63) / 64;
   static_assert(N % 2 == 0, "Hermitian half spectra assume an even length");
@@ -266,6 +270,7 @@ struct EngF500 {
   static constexpr int NJ = 8;
   static constexpr int NH = 5;
   static constexpr int kWaves = 4;
+  static constexpr bool kNextTask = DVH_XPASS_PF != 0;  // the cross-pass prefetch variant takes the next task
   static constexpr size_t kBlockBytes = sizeof(float2) * N;     // twiddle table
   static constexpr size_t kWaveBytes = sizeof(float2) * 2 * N;  // ping-pong buffers
   float2* tw;

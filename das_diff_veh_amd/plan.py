@@ -222,6 +222,7 @@ class VsgPlan:
             raise ValueError("time slices outside the window: the passes' t_axis does not match the window's "
                              f"{n_t} samples")
         self._dev = {}
+        self._ws = {}  # device -> stack-launch workspace (vsg.spectra_workspace)
 
     @classmethod
     def from_trajectories(cls, x_axes, t_axes, veh_xs, veh_ts, prm: VsgParams, n_ch: int, n_t: int):
@@ -311,6 +312,7 @@ class DevicePlan:
             self.seg_tab = torch.empty((n, self.R, 2, 2), dtype=torch.int32, device=dev)
         self.status = torch.empty(n, dtype=torch.int32, device=dev)
         self.geoms = None
+        self._ws = {}  # device -> stack-launch workspace, shared by the slices (their launches are stream-ordered)
         if derive:
             self.derive()
 
@@ -512,6 +514,7 @@ class UnitPlan(VsgPlan):
                              f"{n_t} samples")
         self.geoms = None
         self._dev = {}
+        self._ws = {}  # device -> stack-launch workspace (vsg.spectra_workspace)
 
     @classmethod
     def concat(cls, plans):

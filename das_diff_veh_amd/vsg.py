@@ -10,11 +10,33 @@ stream-ordered on the current torch stream and never synchronise.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
 from . import _lib
 from .plan import VsgPlan
+
+# Stack launches at w = 500: DVH_VSG_ENGINE=q selects the four-step engine (EngQ500, experimental, measured
+# slower: DESIGN.md) with a per-pass table of the shared pivot
+# spectra in a workspace; the default is the per-sub-window engine (EngF500).
+_ENGINE = os.environ.get("DVH_VSG_ENGINE", "f500")
+
+
+def spectra_workspace(plan: VsgPlan, device, cache: dict | None = None):
+    """The pivot-spectra workspace of a stack launch (None when the plan's w does not use one)."""
+    if _ENGINE == "f500":
+        return None
+    nbytes = int(_lib.load().dvh_vsg_stack_workspace(plan.n_pass, plan.w))
+    if nbytes <= 0:
+        return None
+    if cache is not None:
+        ws = cache.get(str(device))
+        if ws is None or ws.numel() * 4 < nbytes:
+            ws = cache[str(device)] = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
+        return ws
+    return torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
 
 
 def _check_windows(windows: torch.Tensor, plan: VsgPlan):
@@ -124,26 +146,31 @@ def vsg_stack(windows: torch.Tensor, plan: VsgPlan, schedule: StackSchedule, sca
         out.zero_()
     if scales is None:
         scales = vsg_scales(windows, plan, win_sumsq=win_sumsq)
+    ws = spectra_workspace(plan, windows.device, getattr(plan, "_ws", None))
     _lib.call("dvh_vsg_stack", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
               _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop, plan.flags, _lib.ptr(scales),
               _lib.ptr(order), _lib.ptr(chunk_tab), int(chunk_tab.shape[0]), _lib.ptr(weights), _lib.ptr(out),
-              _lib.stream_of(windows.device))
+              _lib.ptr(ws), _lib.stream_of(windows.device))
     return out
 
 
 def vsg_stack_validated(windows: torch.Tensor, plan: VsgPlan, schedule: StackSchedule, scales: torch.Tensor | None = None,
                         out: torch.Tensor | None = None, accumulate: bool = False,
-                        work: torch.Tensor | None = None) -> torch.Tensor:
+                        work: torch.Tensor | None = None, scan: "UnitScan | None" = None) -> torch.Tensor:
     """vsg_stack plus the windows' validity in the same launch (dvh_vsg_stack_validated): every sample
     of every window [n_ch, n_t] is read once beside the correlations, and a class slot holding a
     pass whose window has a NaN / inf or is all zero becomes NaN -- the reference's data / ||data||_F
     (apis/virtual_shot_gather.py:125) -- without a separate ||window||_F pass.  Needs norm or norm_amp
     (the raw mode's scale is ||data||_F itself: use window_sumsq + vsg_stack).  ``work`` (optional):
-    int32 device buffer of >= n_pass + 1 elements, reused across calls."""
+    int32 device buffer of >= n_window + 1 elements, reused across calls.  ``scan``: the windows of a
+    unit launch (UnitScan; default: one window per pass)."""
     _check_windows(windows, plan)
     if not (plan.flags & 6):
         raise ValueError("validated stacking needs norm or norm_amp; use window_sumsq + vsg_stack")
-    if windows.shape[1] < plan.R:
+    if scan is None and windows.stride(0) == 0:
+        raise ValueError("a unit launch (flat_units) validates its windows through a UnitScan")
+    n_ch = windows.shape[1] if scan is None else scan.n_ch
+    if n_ch < plan.R:
         raise ValueError("windows narrower than the gather")
     pass_tab, seg_tab = plan.device_tables(windows.device)
     order, chunk_tab, weights = schedule.device_tables(windows.device)
@@ -153,13 +180,38 @@ def vsg_stack_validated(windows: torch.Tensor, plan: VsgPlan, schedule: StackSch
         out.zero_()
     if scales is None:
         scales = vsg_scales(windows, plan, validity=False)
-    if work is None or work.numel() < plan.n_pass + 1 or work.dtype != torch.int32:
-        work = torch.empty(plan.n_pass + 1, dtype=torch.int32, device=windows.device)
+    n_win = plan.n_pass if scan is None else scan.n_win
+    if work is None or work.numel() < n_win + 1 or work.dtype != torch.int32:
+        work = torch.empty(n_win + 1, dtype=torch.int32, device=windows.device)
+    stab, uscan = (None, None) if scan is None else scan.device_tables(windows.device)
+    ws = spectra_workspace(plan, windows.device, getattr(plan, "_ws", None))
     _lib.call("dvh_vsg_stack_validated", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
-              windows.shape[1], windows.shape[2], _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop,
+              n_ch, windows.shape[2], _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop,
               plan.flags, _lib.ptr(scales), _lib.ptr(order), _lib.ptr(chunk_tab), int(chunk_tab.shape[0]),
-              schedule.n_slot, _lib.ptr(weights), _lib.ptr(out), _lib.ptr(work), _lib.stream_of(windows.device))
+              schedule.n_slot, _lib.ptr(weights), _lib.ptr(out), _lib.ptr(stab), n_win, _lib.ptr(uscan),
+              _lib.ptr(work), _lib.ptr(ws), _lib.stream_of(windows.device))
     return out
+
+
+class UnitScan:
+    """The windows a unit launch (plan.UnitPlan over flat_units) validates: window s = ``n_ch`` record
+    rows from ``first_row[s]``; unit u takes the validity of window ``unit_window[u]``.  A pass imaged at
+    several pivots is one window, read once per launch (the reference divides the pass's window by
+    ||data||_F in every VirtualShotGather call, apis/virtual_shot_gather.py:125 -- the same value)."""
+
+    def __init__(self, first_row, unit_window, n_ch):
+        self.first_row = np.ascontiguousarray(first_row, dtype=np.int32)
+        self.unit_window = np.ascontiguousarray(unit_window, dtype=np.int32)
+        self.n_win, self.n_ch = int(self.first_row.size), int(n_ch)
+        if self.unit_window.size and (self.unit_window.min() < 0 or self.unit_window.max() >= self.n_win):
+            raise ValueError("unit window index out of range")
+        self._dev = {}
+
+    def device_tables(self, device):
+        key = str(device)
+        if key not in self._dev:
+            self._dev[key] = tuple(torch.from_numpy(a).to(device) for a in (self.first_row, self.unit_window))
+        return self._dev[key]
 
 
 def flat_units(windows: torch.Tensor, plan) -> torch.Tensor:

@@ -79,11 +79,11 @@ int dvh_vsg_gathers(const float* win, int64_t pass_stride, int64_t ch_stride, in
  * With weight[p] = 1 / count[slot] this is sum(images) / len(images) per class
  * (ImagesFromWindows.get_images, apis/imaging_classes.py:106-107; VirtualShotGather.__add__ /
  * __truediv__ apis/virtual_shot_gather.py:195-210).  order[] lists passes grouped by slot;
- * chunk_tab [n_chunk][3] = {begin, end (into order), slot}. */
+ * chunk_tab [n_chunk][3] = {begin, end (into order), slot}.  spec_ws: see dvh_vsg_stack_workspace. */
 int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, const int32_t* pass_tab,
                   const int32_t* seg_tab, int32_t R, int32_t w, int32_t hop, int32_t flags, const float* scales,
                   const int32_t* order, const int32_t* chunk_tab, int32_t n_chunk, const float* weight, float* stack,
-                  void* stream);
+                  void* spec_ws, void* stream);
 
 /* dvh_vsg_stack with the windows' validity decided in the same launch.  The reference divides every
  * window by ||data||_F (preprocessing_window, apis/virtual_shot_gather.py:125), so a NaN / inf
@@ -91,13 +91,25 @@ int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stride, int3
  * its class -- NaN.  This entry reads every sample of every pass's window once, alongside the
  * correlations, and sets stack[slot] to NaN for each slot (< n_slot) holding such a pass; the
  * scales must then come from dvh_vsg_scales WITHOUT win_sumsq.  Requires flags & (norm | norm_amp):
- * with neither, the scale itself is 1 / ||data||_F^2 (use dvh_window_sumsq).  work: device
- * workspace of n_pass + 1 uint32 (per-pass max |x| bit pattern, a work counter), zeroed inside. */
+ * with neither, the scale itself is 1 / ||data||_F^2 (use dvh_window_sumsq).
+ * Scan windows: with scan_tab == NULL window p is pass p (win + p * pass_stride, n_ch rows); a unit
+ * launch (pass stride 0 over one flattened record, each (pass, pivot) unit a "pass") gives instead
+ * n_scan windows of n_ch rows starting at record rows scan_tab[s], and unit_scan[p] = the window
+ * whose validity unit p takes (a pass imaged at several pivots is read once).  work: device
+ * workspace of (scan_tab ? n_scan : n_pass) + 1 uint32 (per-window max |x| bit pattern, a work
+ * counter), zeroed inside. */
 int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, int32_t n_ch,
                             int32_t n_t, const int32_t* pass_tab, const int32_t* seg_tab, int32_t R, int32_t w,
                             int32_t hop, int32_t flags, const float* scales, const int32_t* order,
                             const int32_t* chunk_tab, int32_t n_chunk, int32_t n_slot, const float* weight, float* stack,
-                            uint32_t* work, void* stream);
+                            const int32_t* scan_tab, int32_t n_scan, const int32_t* unit_scan, uint32_t* work,
+                            void* spec_ws, void* stream);
+
+/* Bytes of the spec_ws workspace dvh_vsg_stack / dvh_vsg_stack_validated take for n_pass passes at
+ * window length w: the spectra of every pass's shared pivot slices (w = 500: 12 KiB per pass), which
+ * lets the stack launch transform only receivers on the shared side (EngQ500).  0 when w does not use
+ * it; with spec_ws == NULL the stack entries run the per-sub-window engine instead. */
+int64_t dvh_vsg_stack_workspace(int32_t n_pass, int32_t w);
 
 /* ---------------------------------------------------------------- dispersion (map_fv)
  * Gathers data[B][nch][nt] (strides in elements).  Only the FK bins the (f, k = f / v) queries

@@ -116,18 +116,19 @@ def class_images(windows, slots, n_slot, pivot, start_x, end_x):
 
 def timed_worker(path, first, budget_s):
     """One single-threaded worker of the all-core CPU baseline: gathers of the windows saved in
-    ``path`` (.npz: wins [n, C, T] float32, x_axis, t_axis, vx/vt [n, L], pivot, start_x, end_x),
-    round robin from window ``first``, until ``budget_s`` has elapsed.  Returns (done, seconds)."""
+    ``path`` (.npz: wins [n, C, T] float32, x_axis, t_axis, vx/vt [n, L], pivot, start_x, end_x -- scalars,
+    or one per window for sliding-pivot units), round robin from window ``first``, until ``budget_s`` has
+    elapsed.  Returns (done, seconds)."""
     import time
     z = np.load(path, allow_pickle=False)
     wins, vx, vt = z["wins"], z["vx"], z["vt"]
     x_axis, t_axis = z["x_axis"], z["t_axis"]
-    pivot, start_x, end_x = float(z["pivot"]), float(z["start_x"]), float(z["end_x"])
     n, done = wins.shape[0], 0
+    piv, sx, ex = (np.broadcast_to(np.asarray(z[k], dtype=np.float64), (n,)) for k in ("pivot", "start_x", "end_x"))
     t0 = time.perf_counter()
     while True:
         i = (first + done) % n
-        gather(np.asarray(wins[i], np.float64), x_axis, t_axis, vx[i], vt[i], pivot, start_x, end_x)
+        gather(np.asarray(wins[i], np.float64), x_axis, t_axis, vx[i], vt[i], piv[i], sx[i], ex[i])
         done += 1
         el = time.perf_counter() - t0
         if el >= budget_s:

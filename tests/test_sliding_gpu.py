@@ -165,3 +165,41 @@ def test_sliding_merged_batches(device):
     for j, gs in refs.items():
         assert gio.gather_rel_err(got[j], ovsg.stack(gs)) < TOL, j
     assert len(refs) >= 2
+
+
+def test_sliding_merged_validated(device):
+    """The sliding bench's launch: two batches merged, windows validated in the stack launch through a
+    UnitScan (window per (batch, pass), every unit taking its pass's validity).  Clean windows: the
+    class stacks equal vsg_stack's; a NaN far from every gather in one window makes exactly the slots
+    holding that window's units NaN (the reference's data / ||data||_F, apis/virtual_shot_gather.py:125)."""
+    from das_diff_veh_amd import vsg
+    from das_diff_veh_amd.plan import UnitPlan, VsgParams
+    from das_diff_veh_amd.synth import synth_batch_device
+    w, x, t, trk = _case(device, n=3, seed=14)
+    _, _, _, trk2, _ = synth_batch_device(3, n_ch=300, n_t=8192, pivot=1100.0, seed=15, device=device,
+                                          x_first=0.37, track_half=1500, chunk=1)
+    prm = VsgParams(include_other_side=True, norm=False)
+    pch = np.arange(32, w.shape[1] - 32, 8)
+    p1 = UnitPlan.sliding(x, t, trk, pch, 200.0, prm)
+    p2 = UnitPlan.sliding(x, t, trk2, pch, 200.0, prm)
+    plan = UnitPlan.concat([p1, p2])
+    n, C = w.shape[0], w.shape[1]
+    scan = vsg.UnitScan(np.tile(np.arange(n) * C, 2), np.concatenate([p1.unit_window, p2.unit_window + n]), C)
+    slots = np.concatenate([p1.unit_pivot, p2.unit_pivot])
+    sched = vsg.StackSchedule(slots, len(pch), chunk=8)
+    flat = vsg.flat_units(w, plan)
+    ref = vsg.vsg_stack(flat, plan, sched, win_sumsq=vsg.unit_sumsq(vsg.window_sumsq(w), plan)).double().cpu().numpy()
+    sc = vsg.vsg_scales(flat, plan, validity=False)
+    got = vsg.vsg_stack_validated(flat, plan, sched, scales=sc, scan=scan).double().cpu().numpy()
+    used = np.unique(slots)
+    assert np.all(np.isfinite(got[used]))
+    assert max(gio.gather_rel_err(got[j], ref[j]) for j in used) < 1e-5
+    w[1, C - 1, 7] = float("nan")  # the last channel's first samples: outside every gather's slices
+    got = vsg.vsg_stack_validated(flat, plan, sched, scales=sc, scan=scan).double().cpu().numpy()
+    bad = np.unique(slots[np.concatenate([p1.unit_window, p2.unit_window]) == 1])
+    assert bad.size >= 1
+    for j in used:
+        if j in bad:
+            assert np.all(np.isnan(got[j])), j
+        else:
+            assert gio.gather_rel_err(got[j], ref[j]) < 1e-5, j
