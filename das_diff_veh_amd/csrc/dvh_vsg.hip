@@ -33,7 +33,6 @@
 #include <algorithm>
 
 #include "vsg_engines.h"
-#include "vsg_engine_q.h"
 #include "dvh_common.h"
 #include "dvh.h"
 
@@ -44,7 +43,6 @@ constexpr int kBlock = 512;  // sumsq kernel
 // EngF500 fits 4
 template <class E> struct Occ { static constexpr int v = 3; };
 template <> struct Occ<EngF500> { static constexpr int v = 4; };
-template <> struct Occ<EngQ500> { static constexpr int v = 3; };  // 4 KB + 4 x 12 KB LDS per block: 3 blocks per CU
 #ifndef DVH_STACKF_OCC
 #define DVH_STACKF_OCC 0
 #endif
@@ -53,35 +51,27 @@ template <> struct Occ<EngQ500> { static constexpr int v = 3; };  // 4 KB + 4 x 
 template <class E> struct OccF {
   static constexpr int v = DVH_STACKF_OCC ? DVH_STACKF_OCC : (E::kWaves == 4 && E::NFFT <= 500 ? 4 : Occ<E>::v);
 };
-template <> struct OccF<EngQ500> { static constexpr int v = Occ<EngQ500>::v; };
 
-// One row task's cross spectra: EngQ500 takes the launch arguments (its slices are addressed per pass).
+// One row task's cross spectra: EngF500 with a bound pivot-spectra table uses it (stack kernels).
 template <class E>
 __device__ __forceinline__ void engine_spectra(E& eng, const VsgArgs& A, const RowTask& t, const RowTask& tn,
                                                bool has_next, float2 (&Cf)[E::NH], float2 (&Co)[E::NH]) {
   eng.spectra(t, tn, has_next, A.w, A.hop, Cf, Co);
 }
 template <>
-__device__ __forceinline__ void engine_spectra<EngQ500>(EngQ500& eng, const VsgArgs& A, const RowTask& t,
-                                                        const RowTask& tn, bool has_next, float2 (&Cf)[EngQ500::NH],
-                                                        float2 (&Co)[EngQ500::NH]) {
-  eng.spectra_q(A, t, t.p, t.row0, eng.ptab, tn, has_next, Cf, Co);
+__device__ __forceinline__ void engine_spectra<EngF500>(EngF500& eng, const VsgArgs& A, const RowTask& t,
+                                                        const RowTask& tn, bool has_next, float2 (&Cf)[EngF500::NH],
+                                                        float2 (&Co)[EngF500::NH]) {
+  if (eng.tab) eng.spectra_tab(t, A.n_pass, A.hop, Cf, Co);
+  else eng.spectra(t, tn, has_next, A.w, A.hop, Cf, Co);
 }
 
-// max |x| bit pattern over what the last spectra call loaded (engines that validate their slices)
+// Engines that read a per-pass table besides the windows (EngF500: the pivot-slice spectra) get it here.
 template <class E>
-__device__ __forceinline__ uint32_t engine_vmax(const E&) { return 0u; }
+__device__ __forceinline__ void bind_engine(E&, const float2*) {}
 template <>
-__device__ __forceinline__ uint32_t engine_vmax<EngQ500>(const EngQ500& e) { return e.vmax; }
-template <>
-__device__ __forceinline__ uint32_t engine_vmax<EngF500>(const EngF500& e) { return e.rmax; }
-
-// Engines that read per-pass tables besides the windows (EngQ500: the shared pivot spectra) get them here.
-template <class E>
-__device__ __forceinline__ void bind_engine(E&, const VsgArgs&, const float2*) {}
-template <>
-__device__ __forceinline__ void bind_engine<EngQ500>(EngQ500& e, const VsgArgs&, const float2* ptab) {
-  e.ptab = ptab;
+__device__ __forceinline__ void bind_engine<EngF500>(EngF500& e, const float2* tab) {
+  e.tab = tab;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -384,8 +374,7 @@ template <class E>
 __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
-                                             float* __restrict__ stack, int64_t t0, int64_t stride,
-                                             uint32_t* __restrict__ vflag = nullptr) {
+                                             float* __restrict__ stack, int64_t t0, int64_t stride) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -409,7 +398,6 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
 #pragma unroll
     for (int m = 0; m < NH; ++m) Gh[m] = make_float2(0.f, 0.f);
     RowTask task = (E::kNextTask && b < e) ? make_task(A, uni(order[b]), i) : RowTask{};
-    uint32_t vmine = 0;  // validated launch, skipping scan: lane k holds max |x| of the chunk's k-th pass's slices
     for (int q = b; q < e; ++q) {
       const int p = uni(order[q]);
       RowTask tn = task;
@@ -423,14 +411,6 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
       }
       float2 Cf[NH], Co[NH];
       engine_spectra(eng, A, task, tn, has_next, Cf, Co);
-      if (vflag) {  // the receiver slices this task loaded are validated here; the scan skips them
-        const uint32_t m = uni((int)wave_max_u32(engine_vmax(eng)));
-        if (q - b < 64) {
-          if (lane_ == q - b) vmine = max(vmine, m);
-        } else if (lane_ == 0) {
-          atomicMax(vflag + p, m);
-        }
-      }
       const float sf = unif(scales[2 * p]), so = unif(scales[2 * p + 1]), wp = unif(weight[p]);
       // per-pass bin / twiddle-index math recomputed here (hoisted, it only spills)
       const int lane = opaque(lane_);
@@ -500,7 +480,6 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
       }
       task = tn;
     }
-    if (vflag && lane_ < min(e - b, 64)) atomicMax(vflag + order[b + lane_], vmine);
     float2 Z[NH];
 #pragma unroll
     for (int m = 0; m < NH; ++m) Z[m] = make_float2(0.f, 0.f);
@@ -522,16 +501,16 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
     float* __restrict__ stack, const float2* __restrict__ ptab) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
-  bind_engine(eng, A, ptab);
+  bind_engine(eng, ptab);
   const int wave = threadIdx.x >> 6;
   stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave,
                   (int64_t)gridDim.x * E::kWaves);
 }
 
-// Spectra of the pivot's shared-window slices of every pass (EngQ500's table): one wave per pass
-// transforms the pivot row's slices pairwise per side (forward q = 0, 1 | 2 and other q = 0, 1 | 2;
-// sides never share a transform) and writes P[f], f <= 250, with the slice's non-zero flag at bin 255.
-__global__ __launch_bounds__(256) void vsg_pivot_spectra_kernel(VsgArgs A, float2* __restrict__ ptab) {
+// The pivot-slice spectra table of every pass (EngF500::spectra_tab): one wave per pass forms the
+// entries' (start, nwin) from the pivot row and the first / last gather rows and transforms their slices
+// pairwise with the Stockham FFT, writing P[f], f <= 250, and each slice's non-zero flag at bin 255.
+__global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float2* tw = reinterpret_cast<float2*>(lds);
   init_twiddles<500>(tw);
@@ -539,51 +518,59 @@ __global__ __launch_bounds__(256) void vsg_pivot_spectra_kernel(VsgArgs A, float
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float2* bufA = reinterpret_cast<float2*>(lds + sizeof(float2) * 500 + (size_t)wave * sizeof(float2) * 1000);
   float2* bufB = bufA + 500;
+  int32_t* head = reinterpret_cast<int32_t*>(tab + (int64_t)A.n_pass * kTabPassF2);
   for (int p = blockIdx.x * 4 + wave; p < A.n_pass; p += gridDim.x * 4) {
     const int row0 = uni(A.pass_tab[2 * p]), pivot = uni(A.pass_tab[2 * p + 1]);
-    const RowTask t = make_task(A, p, pivot - row0);  // the pivot row: both sides shared
+    const RowTask tp = make_task(A, p, pivot - row0), tl = make_task(A, p, A.R - 1), t0 = make_task(A, p, 0);
+    int st[kTabEnt], nw[kTabEnt];
+    st[0] = tp.a_f;
+    nw[0] = tp.nwin_f;
+    st[1] = tp.a_o;
+    nw[1] = tp.nwin_o;
+    st[2] = tl.a_f;
+    nw[2] = tl.ch > pivot ? tl.nwin_f : 0;
+    st[3] = t0.a_o;
+    nw[3] = t0.ch < pivot ? t0.nwin_o : 0;
+    if (lane < 2 * kTabEnt) head[(int64_t)p * 2 * kTabEnt + lane] = (lane & 1) ? nw[lane >> 1] : st[lane >> 1];
+    // the slices (e, q), q < 3, two per transform; absent ones are zero
 #pragma unroll 1
-    for (int side = 0; side < 2; ++side) {
-      const int nw = side == 0 ? t.nwin_f : t.nwin_o;
-      const int a = side == 0 ? t.a_f : t.a_o;
-#pragma unroll 1
-      for (int q0 = 0; q0 < 3; q0 += 2) {
-        const int q1 = q0 + 1;
-        const bool h0 = q0 < nw, h1 = q1 < 3 && q1 < nw;
-        float2* o0 = ptab + ((int64_t)p * 6 + side * 3 + q0) * kPtabBins;
-        float2* o1 = ptab + ((int64_t)p * 6 + side * 3 + (q1 < 3 ? q1 : q0)) * kPtabBins;
-        uint32_t nz0 = 0, nz1 = 0;
-        const float2* X = nullptr;
-        if (h0 || h1) {
-          for (int n = lane; n < 500; n += 64) {
-            const float x0 = h0 ? t.piv[a + q0 * A.hop + n] : 0.f;
-            const float x1 = h1 ? t.piv[a + q1 * A.hop + n] : 0.f;
-            nz0 |= nzbits(x0);
-            nz1 |= nzbits(x1);
-            bufA[n] = make_float2(x0, x1);
-          }
-          wave_sync();
-          X = FftPlan<500>::T::run(bufA, bufB, tw, lane);
-        }
-        const bool l0 = __ballot(nz0 != 0) != 0, l1 = __ballot(nz1 != 0) != 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int f = lane + 64 * j;
-          float2 p0 = make_float2(0.f, 0.f), p1 = p0;
-          if (X && f <= 250) {
-            const float2 za = X[f], zc = X[f == 0 ? 0 : 500 - f];
-            p0 = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y - zc.y));
-            p1 = make_float2(0.5f * (za.y + zc.y), -0.5f * (za.x - zc.x));
-          }
-          if (f == kPtabBins - 1) {
-            p0 = make_float2(l0 ? 1.f : 0.f, 0.f);
-            p1 = make_float2(l1 ? 1.f : 0.f, 0.f);
-          }
-          o0[f] = p0;
-          if (q1 < 3) o1[f] = p1;
+    for (int s0 = 0; s0 < 3 * kTabEnt; s0 += 2) {
+      const int e0 = s0 / 3, q0 = s0 % 3, e1 = (s0 + 1) / 3, q1 = (s0 + 1) % 3;
+      const bool h0 = q0 < nw[e0], h1 = q1 < nw[e1];
+      const float* x0 = tp.piv + st[e0] + q0 * A.hop;
+      const float* x1 = tp.piv + st[e1] + q1 * A.hop;
+      uint32_t nz0 = 0, nz1 = 0;
+      const float2* X = nullptr;
+      if (h0 || h1) {
+        for (int n = lane; n < 500; n += 64) {
+          const float v0 = h0 ? x0[n] : 0.f, v1 = h1 ? x1[n] : 0.f;
+          nz0 |= nzbits(v0);
+          nz1 |= nzbits(v1);
+          bufA[n] = make_float2(v0, v1);
         }
         wave_sync();
+        X = FftPlan<500>::T::run(bufA, bufB, tw, lane);
       }
+      const bool l0 = __ballot(nz0 != 0) != 0, l1 = __ballot(nz1 != 0) != 0;
+      float2* o0 = tab + (((int64_t)p * kTabEnt + e0) * 3 + q0) * kTabBins;
+      float2* o1 = tab + (((int64_t)p * kTabEnt + e1) * 3 + q1) * kTabBins;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int f = lane + 64 * j;
+        float2 p0 = make_float2(0.f, 0.f), p1 = p0;
+        if (X && f <= 250) {
+          const float2 za = X[f], zc = X[f == 0 ? 0 : 500 - f];
+          p0 = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y - zc.y));
+          p1 = make_float2(0.5f * (za.y + zc.y), -0.5f * (za.x - zc.x));
+        }
+        if (f == kTabBins - 1) {
+          p0 = make_float2(l0 ? 1.f : 0.f, 0.f);
+          p1 = make_float2(l1 ? 1.f : 0.f, 0.f);
+        }
+        o0[f] = p0;
+        o1[f] = p1;
+      }
+      wave_sync();
     }
   }
 }
@@ -674,73 +661,7 @@ struct ScanArgs {
   const int32_t* tab;  // nullptr: window s = pass s; else first record row of window s
   int32_t n_win;       // scan windows
   int32_t n_ch, n_t;   // rows and samples of one window
-  int32_t skip;        // 1: skip the receiver slices the correlation waves validate (window s = pass s)
 };
-
-// The sample range [lo, hi) of row c of pass p that the correlation waves load (the row's receiver
-// slices: each side's sub-windows [a, a + (nwin - 1) hop + w)), shrunk to whole float4; both empty
-// outside the gather and on the pivot row (whose shared slices the table kernel reads, unvalidated).
-__device__ __forceinline__ void skip_ranges(const VsgArgs& A, int p, int c, int& lo1, int& hi1, int& lo2, int& hi2) {
-  lo1 = hi1 = lo2 = hi2 = 0;
-  const int row0 = uni(A.pass_tab[2 * p]), pivot = uni(A.pass_tab[2 * p + 1]);
-  const int i = c - row0;
-  if (i < 0 || i >= A.R || c == pivot) return;
-  const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
-  const int nf = n_subwin(uni(seg[1]), A.w, A.hop);
-  if (nf > 0) {
-    const int a = uni(seg[0]);
-    lo1 = (a + 3) & ~3;
-    hi1 = (a + (nf - 1) * A.hop + A.w) & ~3;
-  }
-  const int no = (A.flags & kFlagOtherSide) ? n_subwin(uni(seg[3]), A.w, A.hop) : 0;
-  if (no > 0) {
-    const int a = uni(seg[2]);
-    lo2 = (a + 3) & ~3;
-    hi2 = (a + (no - 1) * A.hop + A.w) & ~3;
-  }
-}
-
-// scan_span over the contiguous rows [c0, c1) of pass p's window, with the loads of each row's receiver
-// slices replaced by out-of-range offsets (no memory request, zero): those samples were validated by the
-// correlation waves.  n_t is a multiple of 16 KB / 4 (16 wave loads of 1 KB), so every batch of kScanDepth
-// loads lies in one row; each row's ranges are fetched one row ahead.
-__device__ __forceinline__ uint32_t scan_rows_skip(const VsgArgs& A, int p, const float* __restrict__ base, int c0,
-                                                   int c1, int n_t, int lane) {
-  const int cpr = n_t >> 8;  // 1 KB chunks per row (a multiple of kScanDepth)
-  const int nch = (c1 - c0) * cpr;
-  const __amdgpu_buffer_rsrc_t rs = scan_rsrc(base + (int64_t)c0 * n_t, (uint32_t)((c1 - c0) * n_t) * 4u);
-  int cur[4], nxt[4];
-  skip_ranges(A, p, c0, cur[0], cur[1], cur[2], cur[3]);
-  skip_ranges(A, p, c0 + 1 < c1 ? c0 + 1 : c0, nxt[0], nxt[1], nxt[2], nxt[3]);
-  int row = 0;
-  auto off = [&](int ch, const int (&g)[4]) -> int {
-    const int col = (ch - row * cpr) * 256 + lane * 4;
-    const bool sk = (col >= g[0] && col + 4 <= g[1]) || (col >= g[2] && col + 4 <= g[3]);
-    return sk ? 0x7ffffff0 : ch * 1024 + lane * 16;
-  };
-  uint32_t m = 0;
-  u32x4 r[kScanDepth];
-#pragma unroll
-  for (int d = 0; d < kScanDepth; ++d) r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off(d, cur), 0, kScanAux);
-  for (int s0 = 0; s0 < nch; s0 += kScanDepth) {
-    const int c = s0 + kScanDepth;  // first chunk this batch issues
-    const bool more = c < nch;
-    if (more && c == (row + 1) * cpr) {  // the batch starts a new row: its ranges were fetched a row ago
-      ++row;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
-      const int rn = c0 + row + 1 < c1 ? c0 + row + 1 : c0 + row;
-      skip_ranges(A, p, rn, nxt[0], nxt[1], nxt[2], nxt[3]);
-    }
-#pragma unroll
-    for (int d = 0; d < kScanDepth; ++d) {
-      const u32x4 v = r[d] & 0x7fffffffu;
-      m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
-      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, more ? off(c + d, cur) : 0x7ffffff0, 0, kScanAux);
-    }
-  }
-  return wave_max_u32(m);
-}
 
 // Pull scan units (window, kScanRows channel rows) until none is left; atomicMax into vflag[window].
 __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, uint32_t* __restrict__ vflag,
@@ -750,16 +671,13 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
   const int n_units = S.n_win * upp;
   const bool vec = (S.n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
                    (reinterpret_cast<uintptr_t>(A.win) % 16 == 0);
-  const bool skip = S.skip && !S.tab && vec && A.ch_stride == S.n_t && S.n_t % (256 * kScanDepth) == 0 &&
-                    (int64_t)S.n_ch * S.n_t < (1ll << 29);
   int u = pull_unit(counter, lane);
   while (u < n_units) {
     const int un = pull_unit(counter, lane);  // the next unit's index, fetched under this unit's loads
     const int q = u / upp, c0 = (u - q * upp) * kScanRows;
     const int s = (sorder && !S.tab) ? uni(sorder[q]) : q;
     const float* base = S.tab ? A.win + (int64_t)uni(S.tab[s]) * A.ch_stride : A.win + (int64_t)s * A.pass_stride;
-    const uint32_t m = skip ? scan_rows_skip(A, s, base, c0, min(c0 + kScanRows, S.n_ch), S.n_t, lane)
-                            : scan_rows(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
+    const uint32_t m = scan_rows(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
     if (lane == 0) atomicMax(vflag + s, m);
     u = un;
   }
@@ -779,14 +697,14 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     const float2* __restrict__ ptab) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
-  bind_engine(eng, A, ptab);
+  bind_engine(eng, ptab);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (wave < kFft) {
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
 #endif
     stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
-                    (int64_t)gridDim.x * kFft, S.skip ? vflag : nullptr);
+                    (int64_t)gridDim.x * kFft);
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1008,31 +926,20 @@ static int cu_count() {
 #ifndef DVH_VSTACK_SCAN
 #define DVH_VSTACK_SCAN 1  // scan waves per block
 #endif
-#ifndef DVH_SCAN_SKIP
-#define DVH_SCAN_SKIP 0  // 1: the validated launch's scan skips the receiver slices the correlation validates
-#endif
-#ifndef DVH_QSTACK_FFT
-#define DVH_QSTACK_FFT 5  // EngQ500: correlation waves per validated block (12 KB of LDS each), 2 blocks per CU
-#endif
-#ifndef DVH_QSTACK_SCAN
-#define DVH_QSTACK_SCAN 1
+#ifndef DVH_PIVOT_TABLE
+#define DVH_PIVOT_TABLE 1  // stack launches at w = 500 with the per-pass pivot-slice spectra table
 #endif
 
-// EngQ500 (the four-step engine with the per-pass pivot spectra table) takes w = N = 500 when the
-// caller gives the table's workspace and a pass's gather rows are addressable by 31-bit byte offsets
-static bool use_q(int n, const VsgArgs& A, const void* ws) {
-  return n == 500 && ws != nullptr && (int64_t)A.R * A.ch_stride * 4 < (1ll << 31) && A.ch_stride >= 0;
-}
-
-static int launch_ptab(VsgArgs& A, float2* ptab, hipStream_t s) {
+static int launch_table(VsgArgs& A, float2* tab, hipStream_t s) {
   const int grid = (int)std::min<int64_t>(((int64_t)A.n_pass + 3) / 4, 8 * (int64_t)cu_count());
-  void* args[] = {&A, &ptab};
-  return launch((const void*)vsg_pivot_spectra_kernel, grid, 4, sizeof(float2) * (500 + 4 * 1000), args, s);
+  void* args[] = {&A, &tab};
+  return launch((const void*)vsg_pivot_table_kernel, grid, 4, sizeof(float2) * (500 + 4 * 1000), args, s);
 }
 
 DVH_API int64_t dvh_vsg_stack_workspace(int32_t n_pass, int32_t w) {
   bool pad;
-  return (choose_fft(w, &pad) == 500 && n_pass > 0) ? (int64_t)n_pass * kPtabPerPass * (int64_t)sizeof(float2) : 0;
+  if (choose_fft(w, &pad) != 500 || n_pass <= 0) return 0;
+  return (int64_t)n_pass * (kTabPassF2 * (int64_t)sizeof(float2) + 2 * kTabEnt * (int64_t)sizeof(int32_t));
 }
 
 DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass,
@@ -1052,37 +959,29 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   VsgKernels k;
   int n;
   if (!get_kernels(w, &k, &n)) return set_error(-4, "unsupported correlation window length");
-  ScanArgs S{scan_tab, scan_tab ? n_scan : n_pass, n_ch, n_t, 0};
+  const ScanArgs S{scan_tab, scan_tab ? n_scan : n_pass, n_ch, n_t};
   hipStream_t s = (hipStream_t)stream;
   uint32_t* vflag = work;
   uint32_t* counter = work + S.n_win;
-  float2* ptab = reinterpret_cast<float2*>(spec_ws);
+  float2* tab = (n == 500 && DVH_PIVOT_TABLE) ? reinterpret_cast<float2*>(spec_ws) : nullptr;
   hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t) * ((size_t)S.n_win + 1), s);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+  if (tab)
+    if (int rc = launch_table(A, tab, s)) return rc;
   const int64_t tasks = (int64_t)n_chunk * R;
   if (n == 500 && DVH_FREQ_STACK) {
-    const bool q = use_q(n, A, spec_ws);
-    if (q) {
-      if (int rc = launch_ptab(A, ptab, s)) return rc;
-      S.skip = DVH_SCAN_SKIP && !scan_tab;  // EngQ500 validates the receiver slices it loads
-    } else {
-      ptab = nullptr;
-      S.skip = DVH_SCAN_SKIP && !scan_tab;  // EngF500 validates the receiver slices it loads (rmax)
-    }
-    const int F = q ? DVH_QSTACK_FFT : DVH_VSTACK_FFT, SC = q ? DVH_QSTACK_SCAN : DVH_VSTACK_SCAN;
-    const void* fn = q ? (const void*)vsg_stackv_kernel<EngQ500, DVH_QSTACK_FFT, DVH_QSTACK_SCAN, 3>
-                       : (const void*)vsg_stackv_kernel<EngF500, DVH_VSTACK_FFT, DVH_VSTACK_SCAN, 4>;
-    const size_t lds = q ? EngQ500::kBlockBytes + F * EngQ500::kWaveBytes : EngF500::kBlockBytes + F * EngF500::kWaveBytes;
+    constexpr int F = DVH_VSTACK_FFT, SC = DVH_VSTACK_SCAN;
+    const void* fn = (const void*)vsg_stackv_kernel<EngF500, F, SC, 4>;
+    const size_t lds = EngF500::kBlockBytes + F * EngF500::kWaveBytes;
     const int64_t need = (tasks + F - 1) / F;
     const int grid = (int)(need < 2 * cu_count() ? (need > 0 ? need : 1) : 2 * cu_count());
-    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &ptab};
+    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &tab};
     if (int rc = launch(fn, grid, F + SC, lds, args, s)) return rc;
   } else {  // other engines: the scan as its own launch, then the plain stack launch
     void* sargs[] = {&A, (void*)&S, &vflag, &counter};
     if (int rc = launch((const void*)window_scan_kernel, 4 * cu_count(), 4, 0, sargs, s)) return rc;
     const int64_t grid = (tasks + k.waves - 1) / k.waves;
-    ptab = nullptr;
-    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &ptab};
+    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &tab};
     if (int rc = launch(k.stack, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, s)) return rc;
   }
   if (n_slot <= 0 || n_chunk <= 0) return 0;
@@ -1105,18 +1004,10 @@ DVH_API int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stri
   if (!get_kernels(w, &k, &n)) return set_error(-4, "unsupported correlation window length");
   const int64_t tasks = (int64_t)n_chunk * R;
   hipStream_t s = (hipStream_t)stream;
-  float2* ptab = nullptr;
-  const void* fn = k.stack;
-  int waves = k.waves;
-  size_t lds = k.lds;
-  if (DVH_FREQ_STACK && use_q(n, A, spec_ws)) {
-    ptab = reinterpret_cast<float2*>(spec_ws);
-    if (int rc = launch_ptab(A, ptab, s)) return rc;
-    fn = (const void*)vsg_stackf_kernel<EngQ500>;
-    waves = EngQ500::kWaves;
-    lds = EngQ500::kBlockBytes + EngQ500::kWaves * EngQ500::kWaveBytes;
-  }
-  const int64_t grid = (tasks + waves - 1) / waves;
-  void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &ptab};
-  return launch(fn, (int)(grid > (1 << 30) ? (1 << 30) : grid), waves, lds, args, s);
+  float2* tab = (n == 500 && DVH_PIVOT_TABLE && DVH_FREQ_STACK) ? reinterpret_cast<float2*>(spec_ws) : nullptr;
+  if (tab)
+    if (int rc = launch_table(A, tab, s)) return rc;
+  const int64_t grid = (tasks + k.waves - 1) / k.waves;
+  void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &tab};
+  return launch(k.stack, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, s);
 }

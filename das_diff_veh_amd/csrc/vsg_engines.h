@@ -17,8 +17,7 @@
 //                        linear correlation folded back to circular in c().
 //   EngF500              N = w = 500 (wlen = 2 s at 250 Hz, the reference's operating point): the
 //                        4 x 5 x 5 x 5 Stockham transform with its first and last stages in registers.
-// (Engine variants measured and not kept -- 20 x 25 register transform, paired in-place 20 x 5 x 5,
-// register twiddles -- are kept for reference in tools/variants/vsg_engine_variants.h.)
+// (Engine variants measured and not kept are listed in DESIGN.md.)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,26 +25,9 @@
 #include "fft_wave.h"
 #include "tw_tables.h"
 
-#ifndef DVH_RCV_AHEAD
-#define DVH_RCV_AHEAD 1  // sub-windows of receiver samples EngF500 keeps in flight (1 or 2)
-#endif
 
 namespace dvh {
 
-#ifndef DVH_XPASS_PF
-#define DVH_XPASS_PF 0  // EngF500: prefetch the next task's first sub-window during the last transform of a call
-#endif
-#ifndef DVH_RCV_NT
-#define DVH_RCV_NT 0  // 1: receiver samples (read once per (pass, row)) loaded non-temporal, sparing the L2 lines
-                      // of the pivot channel every row of a chunk re-reads
-#endif
-__device__ __forceinline__ float rcv_load(const float* p) {
-#if DVH_RCV_NT
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
 
 enum : int32_t {
   kFlagOtherSide = 1,
@@ -255,6 +237,29 @@ struct EngStockham {
 };
 
 // ------------------------------------------------------------------------------------------------
+// Per-pass table of pivot-slice spectra (EngF500::spectra_tab).  A pass's rows read the pivot channel at
+// few distinct slices: every row of a shared side (channel <= pivot forward, >= pivot other side,
+// apis/virtual_shot_gather.py:145-180) at the pivot's own time window, and the trajectory rows whose
+// trajectory time lies outside the record at the clamped window (argmax of an all-False mask is 0,
+// virtual_shot_gather.py:29, so they all slice [0, nsamp)).  Entry e of pass p holds the spectra of the
+// slices [start_e + q hop, + w), q < nwin_e:
+//   e = 0: the forward shared window (the pivot row's forward slice), e = 1: the other side's,
+//   e = 2: the forward trajectory window of the last gather row, e = 3: the other-side trajectory window
+//   of the first gather row (the far rows' clamped windows).
+// A row side whose (start, nwin) equals its entry's transforms only its receivers, two per complex FFT.
+constexpr int kTabEnt = 4;
+constexpr int kTabBins = 256;  // bins f <= 250; [255].x = 1 when the slice has a non-zero sample
+constexpr int64_t kTabPassF2 = (int64_t)kTabEnt * 3 * kTabBins;  // float2 per pass
+
+__device__ __forceinline__ const float2* tab_slice(const float2* tab, int p, int e, int q) {
+  return tab + (((int64_t)p * kTabEnt + e) * 3 + q) * kTabBins;
+}
+// (start, nwin) of every entry: int32 [n_pass][kTabEnt][2] after the spectra
+__device__ __forceinline__ const int32_t* tab_head(const float2* tab, int n_pass) {
+  return reinterpret_cast<const int32_t*>(tab + (int64_t)n_pass * kTabPassF2);
+}
+
+// ------------------------------------------------------------------------------------------------
 // EngF500: N = w = 500 Stockham (4 x 5 x 5 x 5) with the first and last stages fused into registers.
 //   stage 1 (radix 4, span 1) reads its inputs straight from the prefetched sub-window samples
 //     (lane i < 125 of round r holds samples i + 125 t) -- no LDS store of the raw window;
@@ -264,13 +269,19 @@ struct EngStockham {
 //     five bins in registers -- no LDS write of the spectrum and no partner reads.
 // Half-spectrum slots per lane l: j < 3 -> f = l + 100 j (l <= 50); j = 3, 4 -> f = 100 - l + 100 (j - 3)
 // (1 <= l <= 49): each of the 251 bins f <= 250 exactly once.
+//
+// spectra(): one complex transform per sub-window, z = pivot + i receiver.  spectra_tab() (the stack
+// kernels, with the per-pass table above): the sub-windows whose pivot slices are in the table cost only
+// their receivers, packed two per transform (z = R_a + i R_b, separated in stage 4 and multiplied into
+// the table's P conj(R)); the others keep z = P + i R.  On the configs[2] geometry that is 2 transforms
+// for a row whose only side is shared and 3 for a far row with both sides, against 3 and 6.
 struct EngF500 {
   static constexpr int N = 500;
   static constexpr int NFFT = 500;
   static constexpr int NJ = 8;
   static constexpr int NH = 5;
   static constexpr int kWaves = 4;
-  static constexpr bool kNextTask = DVH_XPASS_PF != 0;  // the cross-pass prefetch variant takes the next task
+  static constexpr bool kNextTask = false;
   static constexpr size_t kBlockBytes = sizeof(float2) * N;     // twiddle table
   static constexpr size_t kWaveBytes = sizeof(float2) * 2 * N;  // ping-pong buffers
   float2* tw;
@@ -279,6 +290,7 @@ struct EngF500 {
   int lane;
   bool live_f, live_o;
   uint32_t rmax;  // this lane's max |receiver sample| bit pattern over the last spectra() call
+  const float2* tab = nullptr;  // the pass table of pivot spectra (stack kernels), or none
 
   __device__ EngF500(char* lds, int wave, int lane_) : lane(lane_), live_f(false), live_o(false), rmax(0) {
     tw = reinterpret_cast<float2*>(lds);
@@ -293,17 +305,21 @@ struct EngF500 {
   }
   static __device__ __forceinline__ int slot(int n) { return n; }
 
-  // stage-1 operands of a sub-window starting at a: z[4 r + t] = (pivot, receiver)[i + 125 t], i = lane + 64 r
-  __device__ __forceinline__ void load(const RowTask& t, int a, float2 (&z)[8]) const {
+  // stage-1 operands z[4 r + t] = (re, im)[i + 125 t], i = lane + 64 r, of the slices starting at re / im
+  // (im == nullptr: zeros)
+  __device__ __forceinline__ void load_ri(const float* re, const float* im, float2 (&z)[8]) const {
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int i = lane + 64 * r;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int n = a + i + 125 * u;
-        z[4 * r + u] = (i < 125) ? make_float2(t.piv[n], rcv_load(t.rcv + n)) : make_float2(0.f, 0.f);
+        const int n = i + 125 * u;
+        z[4 * r + u] = (i < 125) ? make_float2(re[n], im ? im[n] : 0.f) : make_float2(0.f, 0.f);
       }
     }
+  }
+  __device__ __forceinline__ void load(const RowTask& t, int a, float2 (&z)[8]) const {
+    load_ri(t.piv + a, t.rcv + a, z);
   }
 
   __device__ __forceinline__ void stage1(const float2 (&z)[8]) const {
@@ -359,7 +375,6 @@ struct EngF500 {
   __device__ __forceinline__ void last_bfly_from(const float2* src, int k, float2 (&x)[5]) const {
 #pragma unroll
     for (int t = 0; t < 5; ++t) x[t] = lds_ld(src, k + 100 * t);
-#if DVH_TW_RECUR
     const float2 w1 = tw[k];
     float2 wt = w1;
 #pragma unroll
@@ -367,42 +382,11 @@ struct EngF500 {
       x[t] = cmul(x[t], wt);
       if (t < 4) wt = cmul(wt, w1);
     }
-#else
-#pragma unroll
-    for (int t = 1; t < 5; ++t) x[t] = cmul(x[t], tw[t * k]);
-#endif
     Dft<5>::run(x);
   }
 
-  // receiver samples of the sub-window starting at a, in load()'s lane layout
-  __device__ __forceinline__ void load_rcv(const RowTask& t, int a, float (&zr)[8]) const {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int i = lane + 64 * r;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) zr[4 * r + u] = (i < 125) ? t.rcv[a + i + 125 * u] : 0.f;
-    }
-  }
-  __device__ __forceinline__ void load_piv(const RowTask& t, int a, float2 (&z)[8]) const {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int i = lane + 64 * r;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) z[4 * r + u].x = (i < 125) ? t.piv[a + i + 125 * u] : 0.f;
-    }
-  }
-
-  // Sub-window q's pivot and receiver samples are loaded one sub-window ahead; with
-  // DVH_RCV_AHEAD == 2 the receiver samples (the HBM-missing stream: pivot slices are shared by the
-  // chunk's rows and mostly hit L2) two sub-windows ahead, for more latency tolerance when the
-  // launch also streams whole windows (vsg_stackv_kernel).  With DVH_XPASS_PF the last sub-window of a
-  // call loads the FIRST sub-window of the caller's next task (tn) into zc, so the first transform of
-  // every pass is prefetched too; a call whose task is not the one prefetched loads its own.
-  float2 zc[8];
-  const float* pre_rcv = nullptr;
-  int pre_a = -1;
-  __device__ void spectra(const RowTask& t, const RowTask& tn, bool has_next, int, int hop, float2 (&Cf)[NH],
-                          float2 (&Co)[NH]) {
+  // Sub-window q's pivot and receiver samples are loaded one sub-window ahead.
+  __device__ void spectra(const RowTask& t, const RowTask&, bool, int, int hop, float2 (&Cf)[NH], float2 (&Co)[NH]) {
     const int nq = t.nwin_f + t.nwin_o;
 #pragma unroll
     for (int j = 0; j < NH; ++j) {
@@ -411,19 +395,8 @@ struct EngF500 {
     }
     live_f = live_o = false;
     auto start = [&](int q) { return q < t.nwin_f ? t.a_f + q * hop : t.a_o + (q - t.nwin_f) * hop; };
-#if DVH_XPASS_PF
-    const int nqn = has_next ? tn.nwin_f + tn.nwin_o : 0;
-    const int an = tn.nwin_f > 0 ? tn.a_f : tn.a_o;
-    if (nq > 0 && !(pre_rcv == t.rcv && pre_a == start(0))) load(t, start(0), zc);
-    pre_rcv = nullptr;
-#else
-    if (nq > 0) load(t, start(0), zc);
-#endif
-    float2 (&z)[8] = zc;
-#if DVH_RCV_AHEAD == 2
-    float zr[8];
-    if (nq > 1) load_rcv(t, start(1), zr);
-#endif
+    float2 z[8];
+    if (nq > 0) load(t, start(0), z);
     rmax = 0;
     for (int q = 0; q < nq; ++q) {
       uint32_t bp = 0, br = 0;
@@ -435,23 +408,7 @@ struct EngF500 {
       }
       const bool live = (__ballot(bp != 0) != 0) && (__ballot(br != 0) != 0);
       if (live) stage1(z);
-      if (q + 1 < nq) {
-#if DVH_RCV_AHEAD == 2
-        load_piv(t, start(q + 1), z);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) z[j].y = zr[j];
-        if (q + 2 < nq) load_rcv(t, start(q + 2), zr);
-#else
-        load(t, start(q + 1), z);
-#endif
-      }
-#if DVH_XPASS_PF
-      else if (nqn > 0) {  // the next task's first sub-window, under this one's stages 2-4
-        load(tn, an, z);
-        pre_rcv = tn.rcv;
-        pre_a = an;
-      }
-#endif
+      if (q + 1 < nq) load(t, start(q + 1), z);
       if (!live) continue;  // exactly zero in the reference
       if (q < t.nwin_f) {
         live_f = true;
@@ -461,13 +418,132 @@ struct EngF500 {
         finish(Co);
       }
     }
-#if DVH_XPASS_PF
-    if (nq == 0 && nqn > 0) {
-      load(tn, an, z);
-      pre_rcv = tn.rcv;
-      pre_a = an;
+  }
+
+  // ---- spectra_tab: the sub-windows whose pivot slices the table holds cost only their receivers ----
+  // Transforms of a row task (wave-uniform): jobs k < npair pack the table-served receivers h = 2k, 2k + 1
+  // (h < nrf: forward side, sub-window h, entry ef; then the other side, entry eo); the remaining nt
+  // trajectory sub-windows (side ts, start at) are z = P + i R as in spectra().
+  struct TabJobs {
+    int nrf, nr, ef, eo, ts, at, nt, npair;
+  };
+  static __device__ __forceinline__ TabJobs tab_jobs(const RowTask& t, const int32_t* head) {
+    TabJobs J;
+    const bool shf = t.ch <= t.pivot, sho = t.ch >= t.pivot;
+    // a trajectory side matches its far-row entry when its slices are the same
+    const bool mf = shf || (t.nwin_f > 0 && t.a_f == uni(head[4]) && t.nwin_f == uni(head[5]));
+    const bool mo = sho || (t.nwin_o > 0 && t.a_o == uni(head[6]) && t.nwin_o == uni(head[7]));
+    J.ef = shf ? 0 : 2;
+    J.eo = sho ? 1 : 3;
+    J.nrf = mf ? t.nwin_f : 0;
+    J.nr = J.nrf + (mo ? t.nwin_o : 0);
+    J.ts = !mf ? 0 : 1;
+    J.nt = !mf ? t.nwin_f : (!mo ? t.nwin_o : 0);
+    J.at = J.ts == 0 ? t.a_f : t.a_o;
+    J.npair = (J.nr + 1) >> 1;
+    return J;
+  }
+  // table-served receiver h: side, sub-window, slice start
+  __device__ __forceinline__ void tab_half(const RowTask& t, const TabJobs& J, int h, int hop, int& side, int& q,
+                                           int& a) const {
+    side = h < J.nrf ? 0 : 1;
+    q = h < J.nrf ? h : h - J.nrf;
+    a = (side == 0 ? t.a_f : t.a_o) + q * hop;
+  }
+  __device__ __forceinline__ void tab_load(const RowTask& t, const TabJobs& J, int k, int hop, float2 (&z)[8]) const {
+    if (k < J.npair) {
+      int s0, q0, a0, s1, q1, a1;
+      tab_half(t, J, 2 * k, hop, s0, q0, a0);
+      tab_half(t, J, 2 * k + 1, hop, s1, q1, a1);
+      load_ri(t.rcv + a0, 2 * k + 1 < J.nr ? t.rcv + a1 : nullptr, z);
+    } else {
+      const int a = J.at + (k - J.npair) * hop;
+      load_ri(t.piv + a, t.rcv + a, z);
     }
-#endif
+  }
+
+  __device__ void spectra_tab(const RowTask& t, int n_pass, int hop, float2 (&Cf)[NH], float2 (&Co)[NH]) {
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      Cf[j] = make_float2(0.f, 0.f);
+      Co[j] = make_float2(0.f, 0.f);
+    }
+    live_f = live_o = false;
+    rmax = 0;
+    const int32_t* head = tab_head(tab, n_pass) + (int64_t)t.p * kTabEnt * 2;
+    const TabJobs J = tab_jobs(t, head);
+    const int nj = J.npair + J.nt;
+    float2 z[8];
+    if (nj > 0) tab_load(t, J, 0, hop, z);
+    for (int k = 0; k < nj; ++k) {
+      const bool pairjob = k < J.npair;
+      uint32_t bp = 0, br = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bp |= nzbits(z[j].x);
+        br |= nzbits(z[j].y);
+        rmax = max(rmax, pairjob ? max(nzbits(z[j].x), nzbits(z[j].y)) : nzbits(z[j].y));
+      }
+      const bool nzp = __ballot(bp != 0) != 0, nzr = __ballot(br != 0) != 0;
+      int s0 = 0, q0 = 0, a0 = 0, s1 = 0, q1 = 0, a1 = 0;
+      bool la = false, lb = false;
+      const float2 *Pa = nullptr, *Pb = nullptr;
+      if (pairjob) {
+        tab_half(t, J, 2 * k, hop, s0, q0, a0);
+        tab_half(t, J, 2 * k + 1, hop, s1, q1, a1);
+        Pa = tab_slice(tab, t.p, s0 == 0 ? J.ef : J.eo, q0);
+        Pb = tab_slice(tab, t.p, s1 == 0 ? J.ef : J.eo, q1);
+        // a receiver slice or its pivot slice identically zero: exactly zero in the reference
+        la = nzp && Pa[kTabBins - 1].x != 0.f;
+        lb = (2 * k + 1 < J.nr) && nzr && Pb[kTabBins - 1].x != 0.f;
+      }
+      const bool live = pairjob ? (la || lb) : (nzp && nzr);
+      if (live) stage1(z);
+      if (k + 1 < nj) tab_load(t, J, k + 1, hop, z);
+      if (!live) continue;
+      if (pairjob) {
+        // the table's P at this lane's bins, loaded under stages 2-3
+        float2 pa[NH], pb[NH];
+#pragma unroll
+        for (int j = 0; j < NH; ++j) {
+          const int f = max(bin(lane, j), 0);
+          pa[j] = Pa[f];
+          pb[j] = Pb[f];
+        }
+        if (la) {
+          if (s0 == 0) live_f = true;
+          else live_o = true;
+        }
+        if (lb) {
+          if (s1 == 0) live_f = true;
+          else live_o = true;
+        }
+        const bool fa = s0 == 0, fb = s1 == 0;
+        finish_with([&](int j, float2 za, float2 zc) {
+          // z = R_a + i R_b: R_a = (Z[f] + conj Z[-f]) / 2, R_b = (Z[f] - conj Z[-f]) / 2i; P conj(R)
+          if (la) {
+            const float2 r = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y - zc.y));
+            const float2 c = make_float2(pa[j].x * r.x + pa[j].y * r.y, pa[j].y * r.x - pa[j].x * r.y);
+            float2& C = fa ? Cf[j] : Co[j];
+            C.x += c.x;
+            C.y += c.y;
+          }
+          if (lb) {
+            const float2 r = make_float2(0.5f * (za.y + zc.y), -0.5f * (za.x - zc.x));
+            const float2 c = make_float2(pb[j].x * r.x + pb[j].y * r.y, pb[j].y * r.x - pb[j].x * r.y);
+            float2& C = fb ? Cf[j] : Co[j];
+            C.x += c.x;
+            C.y += c.y;
+          }
+        });
+      } else if (J.ts == 0) {
+        live_f = true;
+        finish(Cf);
+      } else {
+        live_o = true;
+        finish(Co);
+      }
+    }
   }
 
   __device__ const float2* inverse(const float2 (&Cf)[NH], const float2 (&Co)[NH]) {
@@ -489,6 +565,5 @@ struct EngF500 {
     return make_float2(v.x, -v.y);
   }
 };
-
 
 }  // namespace dvh

@@ -18,15 +18,15 @@ import torch
 from . import _lib
 from .plan import VsgPlan
 
-# Stack launches at w = 500: DVH_VSG_ENGINE=q selects the four-step engine (EngQ500, experimental, measured
-# slower: DESIGN.md) with a per-pass table of the shared pivot
-# spectra in a workspace; the default is the per-sub-window engine (EngF500).
-_ENGINE = os.environ.get("DVH_VSG_ENGINE", "f500")
+# Stack launches at w = 500 take a workspace for the per-pass table of pivot-slice spectra, so that the rows
+# whose pivot slices it holds transform only their receivers (EngF500::spectra_tab); DVH_PIVOT_TABLE=0 runs
+# them without it (every sub-window z = pivot + i receiver; A/B timing).
+_TABLE = os.environ.get("DVH_PIVOT_TABLE", "1") != "0"
 
 
-def spectra_workspace(plan: VsgPlan, device, cache: dict | None = None):
+def spectra_workspace(plan: VsgPlan, device, cache: dict | None = None, table: bool | None = None):
     """The pivot-spectra workspace of a stack launch (None when the plan's w does not use one)."""
-    if _ENGINE == "f500":
+    if not (_TABLE if table is None else table):
         return None
     nbytes = int(_lib.load().dvh_vsg_stack_workspace(plan.n_pass, plan.w))
     if nbytes <= 0:
@@ -134,9 +134,10 @@ class StackSchedule:
 
 def vsg_stack(windows: torch.Tensor, plan: VsgPlan, schedule: StackSchedule, scales: torch.Tensor | None = None,
               out: torch.Tensor | None = None, accumulate: bool = False,
-              win_sumsq: torch.Tensor | None = None) -> torch.Tensor:
+              win_sumsq: torch.Tensor | None = None, table: bool | None = None) -> torch.Tensor:
     """Class-mean gathers [n_slot, R, w]; with accumulate=True adds into ``out``.  ``scales`` come
-    from vsg_scales (formed here with ``win_sumsq`` when not given)."""
+    from vsg_scales (formed here with ``win_sumsq`` when not given).  ``table``: use the pivot-slice
+    spectra table (default: on unless DVH_PIVOT_TABLE=0)."""
     _check_windows(windows, plan)
     pass_tab, seg_tab = plan.device_tables(windows.device)
     order, chunk_tab, weights = schedule.device_tables(windows.device)
@@ -146,7 +147,7 @@ def vsg_stack(windows: torch.Tensor, plan: VsgPlan, schedule: StackSchedule, sca
         out.zero_()
     if scales is None:
         scales = vsg_scales(windows, plan, win_sumsq=win_sumsq)
-    ws = spectra_workspace(plan, windows.device, getattr(plan, "_ws", None))
+    ws = spectra_workspace(plan, windows.device, getattr(plan, "_ws", None), table)
     _lib.call("dvh_vsg_stack", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,
               _lib.ptr(pass_tab), _lib.ptr(seg_tab), plan.R, plan.w, plan.hop, plan.flags, _lib.ptr(scales),
               _lib.ptr(order), _lib.ptr(chunk_tab), int(chunk_tab.shape[0]), _lib.ptr(weights), _lib.ptr(out),

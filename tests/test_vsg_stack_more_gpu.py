@@ -108,3 +108,33 @@ def test_skip_failed_passes_stack_the_rest(device):
     with pytest.raises(ValueError):
         VirtualShotGathersFromWindows(wins).get_images(include_other_side=True, pivot=700, start_x=500, end_x=900,
                                                        wlen=2)
+
+
+@pytest.mark.parametrize("kw", [dict(include_other_side=True, norm=False), dict(include_other_side=True),
+                                dict(include_other_side=False, norm=False)])
+def test_pivot_table_matches_per_subwindow_transforms(device, kw):
+    """The stack launch with the per-pass pivot-slice spectra table (receivers two per transform) equals the
+    per-sub-window transforms (z = pivot + i receiver) on mixed pivot rows and on configs[2]-like far rows
+    (trajectory windows clamped to [0, nsamp): the table's far-row entries)."""
+    from das_diff_veh_amd import vsg
+    from das_diff_veh_amd.plan import VsgParams, VsgPlan, pass_geometry
+    from das_diff_veh_amd.synth import synth_batch_device
+    wins, xs, ts, trk = _mixed_batch(device)
+    prm = VsgParams(**{**KW, **kw})
+    geoms = [pass_geometry(x, t, vx, vt, prm) for x, t, (vx, vt) in zip(xs, ts, trk)]
+    cases = [(wins, VsgPlan(geoms, prm, wins.shape[1], wins.shape[2]))]
+    w, x, t, trk2, _ = synth_batch_device(6, n_ch=256, n_t=4096, pivot=1044.0, seed=31, device=device, x_first=0.0,
+                                          track_half=300, chunk=2)
+    prm2 = VsgParams(pivot=1044.0, start_x=0.0, end_x=2100.0, wlen=2, **kw)
+    geoms2 = [pass_geometry(x, t, vx, vt, prm2) for vx, vt in trk2]
+    cases.append((w, VsgPlan(geoms2, prm2, w.shape[1], w.shape[2])))
+    for wins_c, plan in cases:
+        slots = np.arange(plan.n_pass) % 2
+        sched = vsg.StackSchedule(slots, 2, chunk=4)
+        sc = vsg.vsg_scales(wins_c, plan)
+        a = vsg.vsg_stack(wins_c, plan, sched, scales=sc, table=True).double().cpu().numpy()
+        b = vsg.vsg_stack(wins_c, plan, sched, scales=sc, table=False).double().cpu().numpy()
+        assert np.array_equal(np.isnan(a), np.isnan(b))
+        m = np.isfinite(a)
+        for s in range(2):
+            assert gio.gather_rel_err(np.where(m[s], a[s], 0.0), np.where(m[s], b[s], 0.0)) < 1e-5, (s, kw)
