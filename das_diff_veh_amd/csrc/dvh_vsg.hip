@@ -414,24 +414,30 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
       const float sf = unif(scales[2 * p]), so = unif(scales[2 * p + 1]), wp = unif(weight[p]);
       // per-pass bin / twiddle-index math recomputed here (hoisted, it only spills)
       const int lane = opaque(lane_);
-      bool bad = false, nzo = false;
-      float s2f = 0.f, s2o = 0.f;
+      // sums of |.| over the half spectra: NaN iff some bin is NaN (sums of non-negative values never
+      // turn infinities into NaN); the other side is non-zero iff its sum is
+      float af = 0.f, ao = 0.f;
 #pragma unroll
       for (int m = 0; m < NH; ++m) {
-        const int f = E::bin(lane, m);
-        if (f >= 0) {
-          bad |= isnan(Cf[m].x) || isnan(Cf[m].y) || isnan(Co[m].x) || isnan(Co[m].y);
-          nzo |= (Co[m].x != 0.f) || (Co[m].y != 0.f);
-          // Parseval over all N bins from the half spectrum: interior bins count twice
-          const float wgt = (f == 0 || f == h) ? 1.f : 2.f;
-          s2f += wgt * (Cf[m].x * Cf[m].x + Cf[m].y * Cf[m].y);
-          s2o += wgt * (Co[m].x * Co[m].x + Co[m].y * Co[m].y);
+        if (E::bin(lane, m) >= 0) {
+          af += fabsf(Cf[m].x) + fabsf(Cf[m].y);
+          ao += fabsf(Co[m].x) + fabsf(Co[m].y);
         }
       }
-      bad = __ballot(bad) != 0;
-      nzo = other && (__ballot(nzo) != 0);
+      const bool bad = __ballot(isnan(af + ao)) != 0;
+      const bool nzo = other && (__ballot(ao != 0.f) != 0);
       float ff, fo;
-      if (norm) {  // ||c||^2 = sum_m |C[m]|^2 / N
+      if (norm) {  // ||c||^2 = sum_m |C[m]|^2 / N (Parseval over all N bins: interior bins count twice)
+        float s2f = 0.f, s2o = 0.f;
+#pragma unroll
+        for (int m = 0; m < NH; ++m) {
+          const int f = E::bin(lane, m);
+          if (f >= 0) {
+            const float wgt = (f == 0 || f == h) ? 1.f : 2.f;
+            s2f += wgt * (Cf[m].x * Cf[m].x + Cf[m].y * Cf[m].y);
+            s2o += wgt * (Co[m].x * Co[m].x + Co[m].y * Co[m].y);
+          }
+        }
         ff = sqrtf((float)N) / sqrtf(wave_sum(s2f));
         fo = sqrtf((float)N) / sqrtf(wave_sum(s2o));
       } else {
@@ -453,25 +459,27 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
       } else {
         // other row finite and not identically zero (row_epilogue's test)
         const bool ok = nzo && fo != 0.f;
-        const float cf = wp * (ok ? 0.5f : 1.f) * ff;
-        const float co = ok ? wp * 0.5f * fo : 0.f;
+        // lag shifts as phase ramps W^(s f): forward s = h - 1 on both row types (conj on the shared
+        // window), other side s = h - 1 (shared, conj) or h (trajectory window).  W^(h f) = (-1)^f and
+        // every engine's bins have the lane's parity, so W^((h-1) f) = (-1)^lane conj(tw[f]).
+        const float sg = (lane & 1) ? -1.f : 1.f;
+        const float cf = sg * wp * (ok ? 0.5f : 1.f) * ff;
+        const float co = ok ? sg * wp * 0.5f * fo : 0.f;
         const bool fwd_shared = task.ch <= task.pivot;
         const bool oth_shared = task.ch >= task.pivot;
-        // W^(s m): fwd shared s = w-1-h (conj), fwd traj s = -(h+1); other shared s = h-1 (conj),
-        // other traj s = h
-        const int sf_shift = fwd_shared ? N - 1 - h : N - (h + 1);
-        const int so_shift = oth_shared ? h - 1 : h;
 #pragma unroll
         for (int m = 0; m < NH; ++m) {
           const int f = E::bin(lane, m);
           if (f >= 0) {
+            const float2 t = eng.twiddle(f);
+            const float2 tc = make_float2(t.x, -t.y);
             float2 x = fwd_shared ? make_float2(Cf[m].x, -Cf[m].y) : Cf[m];
-            x = cmul(x, eng.twiddle((sf_shift * f) % N));
+            x = cmul(x, tc);
             Gh[m].x += cf * x.x;
             Gh[m].y += cf * x.y;
             if (ok) {
-              float2 y = oth_shared ? make_float2(Co[m].x, -Co[m].y) : Co[m];
-              y = cmul(y, eng.twiddle((so_shift * f) % N));
+              float2 y = Co[m];
+              if (oth_shared) y = cmul(make_float2(y.x, -y.y), tc);
               Gh[m].x += co * y.x;
               Gh[m].y += co * y.y;
             }

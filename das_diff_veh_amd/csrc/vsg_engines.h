@@ -134,9 +134,8 @@ struct EngStockham {
   float2* bufB;
   int lane;
   bool live_f, live_o;  // some sub-window of the side had non-zero pivot and receiver slices
-  uint32_t rmax;        // this lane's max |receiver sample| bit pattern over the last spectra() call
 
-  __device__ EngStockham(char* lds, int wave, int lane_) : lane(lane_), live_f(false), live_o(false), rmax(0) {
+  __device__ EngStockham(char* lds, int wave, int lane_) : lane(lane_), live_f(false), live_o(false) {
     tw = reinterpret_cast<float2*>(lds);
     bufA = reinterpret_cast<float2*>(lds + kBlockBytes + (size_t)wave * kWaveBytes);
     bufB = bufA + N;
@@ -162,7 +161,6 @@ struct EngStockham {
       Co[j] = make_float2(0.f, 0.f);
     }
     live_f = live_o = false;
-    rmax = 0;
     if (nq > 0) load(t, t.nwin_f > 0 ? t.a_f : t.a_o, w, z);
     for (int q = 0; q < nq; ++q) {
       uint32_t bp = 0, br = 0;
@@ -172,7 +170,6 @@ struct EngStockham {
         if (n < N) bufA[n] = z[j];
         bp |= nzbits(z[j].x);
         br |= nzbits(z[j].y);
-        rmax = max(rmax, nzbits(z[j].y));
       }
       const bool live = (__ballot(bp != 0) != 0) && (__ballot(br != 0) != 0);
       if (q + 1 < nq) {
@@ -289,10 +286,9 @@ struct EngF500 {
   float2* bufB;
   int lane;
   bool live_f, live_o;
-  uint32_t rmax;  // this lane's max |receiver sample| bit pattern over the last spectra() call
   const float2* tab = nullptr;  // the pass table of pivot spectra (stack kernels), or none
 
-  __device__ EngF500(char* lds, int wave, int lane_) : lane(lane_), live_f(false), live_o(false), rmax(0) {
+  __device__ EngF500(char* lds, int wave, int lane_) : lane(lane_), live_f(false), live_o(false) {
     tw = reinterpret_cast<float2*>(lds);
     bufA = reinterpret_cast<float2*>(lds + kBlockBytes + (size_t)wave * kWaveBytes);
     bufB = bufA + N;
@@ -306,15 +302,18 @@ struct EngF500 {
   static __device__ __forceinline__ int slot(int n) { return n; }
 
   // stage-1 operands z[4 r + t] = (re, im)[i + 125 t], i = lane + 64 r, of the slices starting at re / im
-  // (im == nullptr: zeros)
+  // Branch-free: lanes past the 125 stage-1 butterflies (round 1, lane >= 61) load lane 60's samples
+  // again, which stage1() does not store and which leave the non-zero tests unchanged; with im ==
+  // nullptr the receiver is loaded into both halves (the second half's result is discarded).
   __device__ __forceinline__ void load_ri(const float* re, const float* im, float2 (&z)[8]) const {
+    const float* ip = im ? im : re;
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      const int i = lane + 64 * r;
+      const int i = r == 0 ? lane : min(lane + 64, 124);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int n = i + 125 * u;
-        z[4 * r + u] = (i < 125) ? make_float2(re[n], im ? im[n] : 0.f) : make_float2(0.f, 0.f);
+        z[4 * r + u] = make_float2(re[n], ip[n]);
       }
     }
   }
@@ -397,14 +396,12 @@ struct EngF500 {
     auto start = [&](int q) { return q < t.nwin_f ? t.a_f + q * hop : t.a_o + (q - t.nwin_f) * hop; };
     float2 z[8];
     if (nq > 0) load(t, start(0), z);
-    rmax = 0;
     for (int q = 0; q < nq; ++q) {
       uint32_t bp = 0, br = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         bp |= nzbits(z[j].x);
         br |= nzbits(z[j].y);
-        rmax = max(rmax, nzbits(z[j].y));
       }
       const bool live = (__ballot(bp != 0) != 0) && (__ballot(br != 0) != 0);
       if (live) stage1(z);
@@ -469,7 +466,6 @@ struct EngF500 {
       Co[j] = make_float2(0.f, 0.f);
     }
     live_f = live_o = false;
-    rmax = 0;
     const int32_t* head = tab_head(tab, n_pass) + (int64_t)t.p * kTabEnt * 2;
     const TabJobs J = tab_jobs(t, head);
     const int nj = J.npair + J.nt;
@@ -482,7 +478,6 @@ struct EngF500 {
       for (int j = 0; j < 8; ++j) {
         bp |= nzbits(z[j].x);
         br |= nzbits(z[j].y);
-        rmax = max(rmax, pairjob ? max(nzbits(z[j].x), nzbits(z[j].y)) : nzbits(z[j].y));
       }
       const bool nzp = __ballot(bp != 0) != 0, nzr = __ballot(br != 0) != 0;
       int s0 = 0, q0 = 0, a0 = 0, s1 = 0, q1 = 0, a1 = 0;
