@@ -602,7 +602,10 @@ __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2*
 // its windows instead: scan_tab[s] = first record row of window s, and unit_scan[u] = the window whose
 // flag unit u takes, so a pass imaged at several pivots is validated once per launch.
 constexpr int kScanRows = 16;
-constexpr int kScanDepth = 16;
+#ifndef DVH_SCAN_DEPTH
+#define DVH_SCAN_DEPTH 16
+#endif
+constexpr int kScanDepth = DVH_SCAN_DEPTH;  // 16-byte loads per lane in flight
 constexpr int kScanAux = 2;  // cache policy of the scan's buffer loads (nt; allocating loads measured 4 % slower)
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
@@ -934,6 +937,9 @@ static int cu_count() {
 #ifndef DVH_VSTACK_SCAN
 #define DVH_VSTACK_SCAN 1  // scan waves per block
 #endif
+#ifndef DVH_VSTACK_BPC
+#define DVH_VSTACK_BPC 2  // blocks per CU
+#endif
 #ifndef DVH_PIVOT_TABLE
 #define DVH_PIVOT_TABLE 1  // stack launches at w = 500 with the per-pass pivot-slice spectra table
 #endif
@@ -982,7 +988,7 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
     const void* fn = (const void*)vsg_stackv_kernel<EngF500, F, SC, 4>;
     const size_t lds = EngF500::kBlockBytes + F * EngF500::kWaveBytes;
     const int64_t need = (tasks + F - 1) / F;
-    const int grid = (int)(need < 2 * cu_count() ? (need > 0 ? need : 1) : 2 * cu_count());
+    const int grid = (int)(need < DVH_VSTACK_BPC * cu_count() ? (need > 0 ? need : 1) : DVH_VSTACK_BPC * cu_count());
     void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &tab};
     if (int rc = launch(fn, grid, F + SC, lds, args, s)) return rc;
   } else {  // other engines: the scan as its own launch, then the plain stack launch

@@ -141,3 +141,42 @@ def test_validated_stack(batch, refs):
             else:
                 ref = ovsg.stack([refs[i] for i in np.where(slots == s)[0]])
                 assert gio.gather_rel_err(got[s], ref) < TOL, (key, s)
+
+
+def test_validated_stack_receiver_slices(batch, refs):
+    """Window validity inside the slices the correlation waves load (which the launch's scan may leave to
+    them) and in the samples between them: a NaN in a gather row's receiver slice, an inf just past the end
+    of another row's slice and an all-zero window each turn exactly their class NaN."""
+    import torch
+
+    from das_diff_veh_amd.vsg import StackSchedule, vsg_stack_validated
+    from oracle import vsg as ovsg
+    plan = batch["plan"]
+    seg = plan.host_seg_tab().reshape(plan.n_pass, plan.R, 2, 2)  # (start, len) per pass, row, side
+    win = batch["win"]
+    slots = np.array([0, 1, 0, 1, 2, 2])
+    cases = []
+    w = win.clone()  # pass 2 (slot 0): NaN inside row 100's forward receiver slice
+    a, n = int(seg[2, 100, 0, 0]), int(seg[2, 100, 0, 1])
+    assert n >= 500
+    w[2, 100, a + 10] = float("nan")
+    cases.append((w, {0}))
+    w = win.clone()  # pass 3 (slot 1): -inf one sample past the end of row 700's other-side slice
+    a, n = int(seg[3, 700, 1, 0]), int(seg[3, 700, 1, 1])
+    assert n >= 500 and a + n < win.shape[2]
+    w[3, 700, a + n] = float("-inf")
+    cases.append((w, {1}))
+    w = win.clone()  # pass 4 (slot 2): all zero (0 / 0 in the reference)
+    w[4] = 0.0
+    cases.append((w, {2}))
+    for w, bad in cases:
+        torch.cuda.synchronize()
+        got = vsg_stack_validated(w, batch["plan"], StackSchedule(slots, 3, chunk=2)).double().cpu().numpy()
+        for s in range(3):
+            if s in bad:
+                assert np.isnan(got[s]).all(), (bad, s)
+            elif s < 2:
+                ref = ovsg.stack([refs[i] for i in np.where(slots == s)[0]])
+                assert gio.gather_rel_err(got[s], ref) < TOL, (bad, s)
+            else:
+                assert not np.isnan(got[s]).all(), (bad, s)
