@@ -43,6 +43,9 @@ constexpr int kBlock = 512;  // sumsq kernel
 // EngF500 fits 4
 template <class E> struct Occ { static constexpr int v = 3; };
 template <> struct Occ<EngF500> { static constexpr int v = 4; };
+#ifndef DVH_DIRECT
+#define DVH_DIRECT 1  // EngF500 stack kernels: single-sided row tasks transformed across passes (direct_task)
+#endif
 #ifndef DVH_STACKF_OCC
 #define DVH_STACKF_OCC 0
 #endif
@@ -64,6 +67,19 @@ __device__ __forceinline__ void engine_spectra<EngF500>(EngF500& eng, const VsgA
                                                         float2 (&Co)[EngF500::NH]) {
   if (eng.tab) eng.spectra_tab(t, A.n_pass, A.hop, Cf, Co);
   else eng.spectra(t, tn, has_next, A.w, A.hop, Cf, Co);
+}
+
+// A row task whose passes have only a table-served forward side, transformed across passes (EngF500).
+template <class E>
+__device__ __forceinline__ bool engine_direct(E&, const VsgArgs&, const float*, const int32_t*, const float*, int, int,
+                                              int, float2 (&)[E::NH]) {
+  return false;
+}
+template <>
+__device__ __forceinline__ bool engine_direct<EngF500>(EngF500& eng, const VsgArgs& A, const float* scales,
+                                                       const int32_t* order, const float* weight, int b, int e, int i,
+                                                       float2 (&Gh)[EngF500::NH]) {
+  return DVH_DIRECT && eng.tab && eng.direct_task(A, scales, order, weight, b, e, i, Gh);
 }
 
 // Engines that read a per-pass table besides the windows (EngF500: the pivot-slice spectra) get it here.
@@ -280,7 +296,7 @@ __device__ __forceinline__ void gather_row(E& eng, const VsgArgs& A, const float
                                            const RowTask& t, const RowTask& nt, bool has_next, int lane,
                                            float (&G)[E::NJ]) {
   const float2* Y = eng.correlate(t, nt, has_next, A.w, A.hop);
-  row_epilogue<E>(eng, A, Y, t, unif(scales[2 * p]), unif(scales[2 * p + 1]), lane, G);
+  row_epilogue<E>(eng, A, Y, t, sld(scales + 2 * p), sld(scales + 2 * p + 1), lane, G);
 }
 
 template <class E>
@@ -327,28 +343,28 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stack_kernel(V
   const int64_t stride = (int64_t)gridDim.x * E::kWaves;
   for (int64_t t = (int64_t)xcd_block() * E::kWaves + wave; t < n_task; t += stride) {
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
-    const int b = uni(chunk_tab[3 * c]), e = uni(chunk_tab[3 * c + 1]), slot = uni(chunk_tab[3 * c + 2]);
+    const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
     // first pass of the wave's next task (for the cross-task slice prefetch)
     int np = -1, ni = 0;
     if (t + stride < n_task) {
       const int c2 = uni((int)((t + stride) / A.R));
       ni = uni((int)((t + stride) % A.R));
-      const int b2 = uni(chunk_tab[3 * c2]);
-      if (b2 < uni(chunk_tab[3 * c2 + 1])) np = uni(order[b2]);
+      const int b2 = sld(chunk_tab + 3 * c2);
+      if (b2 < sld(chunk_tab + 3 * c2 + 1)) np = sld(order + b2);
     }
     float acc[NJ];
 #pragma unroll
     for (int m = 0; m < NJ; ++m) acc[m] = 0.f;
-    RowTask task = b < e ? make_task(A, uni(order[b]), i) : RowTask{};
+    RowTask task = b < e ? make_task(A, sld(order + b), i) : RowTask{};
     for (int q = b; q < e; ++q) {
-      const int p = uni(order[q]);
+      const int p = sld(order + q);
       RowTask tn = task;
       const bool has_next = (q + 1 < e) || np >= 0;
-      if (q + 1 < e) tn = make_task(A, uni(order[q + 1]), i);
+      if (q + 1 < e) tn = make_task(A, sld(order + q + 1), i);
       else if (np >= 0) tn = make_task(A, np, ni);
       float G[NJ];
       gather_row<E>(eng, A, scales, p, task, tn, has_next, lane, G);
-      const float wp = unif(weight[p]);
+      const float wp = sld(weight + p);
 #pragma unroll
       for (int m = 0; m < NJ; ++m) acc[m] += G[m] * wp;
       task = tn;
@@ -385,33 +401,34 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
   const int64_t n_task = (int64_t)n_chunk * A.R;
   for (int64_t t = t0; t < n_task; t += stride) {
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
-    const int b = uni(chunk_tab[3 * c]), e = uni(chunk_tab[3 * c + 1]), slot = uni(chunk_tab[3 * c + 2]);
+    const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
     int np = -1, ni = 0;
     if (E::kNextTask && t + stride < n_task) {
       const int c2 = uni((int)((t + stride) / A.R));
       ni = uni((int)((t + stride) % A.R));
-      const int b2 = uni(chunk_tab[3 * c2]);
-      if (b2 < uni(chunk_tab[3 * c2 + 1])) np = uni(order[b2]);
+      const int b2 = sld(chunk_tab + 3 * c2);
+      if (b2 < sld(chunk_tab + 3 * c2 + 1)) np = sld(order + b2);
     }
     float* o = stack + ((int64_t)slot * A.R + i) * A.w;
     float2 Gh[NH];
 #pragma unroll
     for (int m = 0; m < NH; ++m) Gh[m] = make_float2(0.f, 0.f);
-    RowTask task = (E::kNextTask && b < e) ? make_task(A, uni(order[b]), i) : RowTask{};
-    for (int q = b; q < e; ++q) {
-      const int p = uni(order[q]);
+    RowTask task = (E::kNextTask && b < e) ? make_task(A, sld(order + b), i) : RowTask{};
+    const bool direct = !norm && engine_direct(eng, A, scales, order, weight, b, e, i, Gh);
+    for (int q = direct ? e : b; q < e; ++q) {
+      const int p = sld(order + q);
       RowTask tn = task;
       bool has_next = false;
       if (E::kNextTask) {  // engines that prefetch the next task's first sub-window get it
         has_next = (q + 1 < e) || np >= 0;
-        if (q + 1 < e) tn = make_task(A, uni(order[q + 1]), i);
+        if (q + 1 < e) tn = make_task(A, sld(order + q + 1), i);
         else if (np >= 0) tn = make_task(A, np, ni);
       } else {
         task = make_task(A, p, i);
       }
       float2 Cf[NH], Co[NH];
       engine_spectra(eng, A, task, tn, has_next, Cf, Co);
-      const float sf = unif(scales[2 * p]), so = unif(scales[2 * p + 1]), wp = unif(weight[p]);
+      const float sf = sld(scales + 2 * p), so = sld(scales + 2 * p + 1), wp = sld(weight + p);
       // per-pass bin / twiddle-index math recomputed here (hoisted, it only spills)
       const int lane = opaque(lane_);
       // sums of |.| over the half spectra: NaN iff some bin is NaN (sums of non-negative values never
@@ -528,7 +545,7 @@ __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2*
   float2* bufB = bufA + 500;
   int32_t* head = reinterpret_cast<int32_t*>(tab + (int64_t)A.n_pass * kTabPassF2);
   for (int p = blockIdx.x * 4 + wave; p < A.n_pass; p += gridDim.x * 4) {
-    const int row0 = uni(A.pass_tab[2 * p]), pivot = uni(A.pass_tab[2 * p + 1]);
+    const int row0 = sld(A.pass_tab + 2 * p), pivot = sld(A.pass_tab + 2 * p + 1);
     const RowTask tp = make_task(A, p, pivot - row0), tl = make_task(A, p, A.R - 1), t0 = make_task(A, p, 0);
     int st[kTabEnt], nw[kTabEnt];
     st[0] = tp.a_f;
@@ -686,8 +703,8 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
   while (u < n_units) {
     const int un = pull_unit(counter, lane);  // the next unit's index, fetched under this unit's loads
     const int q = u / upp, c0 = (u - q * upp) * kScanRows;
-    const int s = (sorder && !S.tab) ? uni(sorder[q]) : q;
-    const float* base = S.tab ? A.win + (int64_t)uni(S.tab[s]) * A.ch_stride : A.win + (int64_t)s * A.pass_stride;
+    const int s = (sorder && !S.tab) ? sld(sorder + q) : q;
+    const float* base = S.tab ? A.win + (int64_t)sld(S.tab + s) * A.ch_stride : A.win + (int64_t)s * A.pass_stride;
     const uint32_t m = scan_rows(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
     if (lane == 0) atomicMax(vflag + s, m);
     u = un;
@@ -721,7 +738,7 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
 #endif
   }
   // the chunks cover order[0, end of the last chunk): scan in that order when it lists every pass
-  const int32_t* sorder = (n_chunk > 0 && uni(chunk_tab[3 * (n_chunk - 1) + 1]) == A.n_pass) ? order : nullptr;
+  const int32_t* sorder = (n_chunk > 0 && sld(chunk_tab + 3 * (n_chunk - 1) + 1) == A.n_pass) ? order : nullptr;
   scan_units(A, S, vflag, counter, lane, sorder);
 }
 

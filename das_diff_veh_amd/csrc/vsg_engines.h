@@ -61,6 +61,15 @@ __device__ __forceinline__ float unif(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
 }
 
+// Wave-uniform load through the scalar cache (s_load).  The tables the kernels read (pass / segment / chunk
+// tables, order, scales, weights, the pivot-spectra table) are written only by earlier launches, so the
+// constant address space is safe; it keeps these dependent loads off the vector memory pipe, where they
+// queued behind the receiver loads.  The address must be wave-uniform.
+template <class T>
+__device__ __forceinline__ T sld(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+
 // Everything a row task needs, wave-uniform.
 struct RowTask {
   const float* piv;
@@ -74,20 +83,20 @@ __device__ __forceinline__ RowTask make_task(const VsgArgs& A, int p, int i) {
   p = uni(p);
   i = uni(i);
   RowTask t;
-  const int row0 = uni(A.pass_tab[2 * p]);
+  const int row0 = sld(A.pass_tab + 2 * p);
   t.p = p;
   t.row0 = row0;
-  t.pivot = uni(A.pass_tab[2 * p + 1]);
+  t.pivot = sld(A.pass_tab + 2 * p + 1);
   t.ch = row0 + i;
   const float* base = A.win + (int64_t)p * A.pass_stride;
   t.piv = base + (int64_t)t.pivot * A.ch_stride;
   t.rcv = base + (int64_t)t.ch * A.ch_stride;
   const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
-  t.a_f = uni(seg[0]);
-  t.nwin_f = n_subwin(uni(seg[1]), A.w, A.hop);
+  t.a_f = sld(seg);
+  t.nwin_f = n_subwin(sld(seg + 1), A.w, A.hop);
   const bool other = (A.flags & kFlagOtherSide) != 0;
-  t.a_o = uni(seg[2]);
-  t.nwin_o = other ? n_subwin(uni(seg[3]), A.w, A.hop) : 0;
+  t.a_o = sld(seg + 2);
+  t.nwin_o = other ? n_subwin(sld(seg + 3), A.w, A.hop) : 0;
   return t;
 }
 
@@ -428,8 +437,8 @@ struct EngF500 {
     TabJobs J;
     const bool shf = t.ch <= t.pivot, sho = t.ch >= t.pivot;
     // a trajectory side matches its far-row entry when its slices are the same
-    const bool mf = shf || (t.nwin_f > 0 && t.a_f == uni(head[4]) && t.nwin_f == uni(head[5]));
-    const bool mo = sho || (t.nwin_o > 0 && t.a_o == uni(head[6]) && t.nwin_o == uni(head[7]));
+    const bool mf = shf || (t.nwin_f > 0 && t.a_f == sld(head + 4) && t.nwin_f == sld(head + 5));
+    const bool mo = sho || (t.nwin_o > 0 && t.a_o == sld(head + 6) && t.nwin_o == sld(head + 7));
     J.ef = shf ? 0 : 2;
     J.eo = sho ? 1 : 3;
     J.nrf = mf ? t.nwin_f : 0;
@@ -489,8 +498,8 @@ struct EngF500 {
         Pa = tab_slice(tab, t.p, s0 == 0 ? J.ef : J.eo, q0);
         Pb = tab_slice(tab, t.p, s1 == 0 ? J.ef : J.eo, q1);
         // a receiver slice or its pivot slice identically zero: exactly zero in the reference
-        la = nzp && Pa[kTabBins - 1].x != 0.f;
-        lb = (2 * k + 1 < J.nr) && nzr && Pb[kTabBins - 1].x != 0.f;
+        la = nzp && sld(&Pa[kTabBins - 1].x) != 0.f;
+        lb = (2 * k + 1 < J.nr) && nzr && sld(&Pb[kTabBins - 1].x) != 0.f;
       }
       const bool live = pairjob ? (la || lb) : (nzp && nzr);
       if (live) stage1(z);
@@ -539,6 +548,149 @@ struct EngF500 {
         finish(Co);
       }
     }
+  }
+
+  // ---- direct_task: a row task whose passes have only a table-served forward side ----
+  // (no row norm; every pass's other side empty, its forward slices in the table, the same sub-window count
+  // W and shared/far-window kind on every pass, finite factors).  The passes' receivers are then packed two
+  // per transform ACROSS passes -- ceil(W n / 2) transforms for n passes instead of n ceil(W / 2) -- and each
+  // pass's weight w_p = weight / W * scale is applied per half:  U = sum_p w_p sum_q P_pq conj(R_pq),
+  // Gh = (-1)^lane ramp(U), the forward epilogue of stackf_tasks (ok = false: no other side) summed over
+  // the passes.  On the configs[2] geometry these are the rows below the pivot (3 receivers per pass).
+  // Returns false (nothing done) when the task does not qualify.
+  __device__ bool direct_task(const VsgArgs& A, const float* __restrict__ scales, const int32_t* __restrict__ order,
+                              const float* __restrict__ weight, int b, int e, int i, float2 (&Gh)[NH]) {
+    const int n = e - b;
+    if (n <= 1 || n > 64) return false;
+    const bool other = (A.flags & kFlagOtherSide) != 0;
+    // lane k < n: pass order[b + k] (the passes' table entries in flight together: one load latency)
+    const bool act = lane < n;
+    int p = 0, row0 = 0, piv = 0, a = 0, L = 0, Lo = 0, h4 = -1, h5 = -1;
+    float sf = 0.f, wp = 0.f;
+    if (act) {
+      p = order[b + lane];
+      row0 = A.pass_tab[2 * p];
+      piv = A.pass_tab[2 * p + 1];
+      const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
+      a = seg[0];
+      L = seg[1];
+      Lo = seg[3];
+      const int32_t* head = tab_head(tab, A.n_pass) + (int64_t)p * kTabEnt * 2;
+      h4 = head[4];
+      h5 = head[5];
+      sf = scales[2 * p];
+      wp = weight[p];
+    }
+    const int ch = row0 + i;
+    const int nwf = n_subwin(L, A.w, A.hop), nwo = other ? n_subwin(Lo, A.w, A.hop) : 0;
+    const bool shf = ch <= piv;
+    const int W = uni(nwf);
+    const bool shf0 = uni(shf ? 1 : 0) != 0;
+    const bool mf = shf || (nwf > 0 && a == h4 && nwf == h5);
+    // the epilogue's forward factor: ff = 1 / nwin_f, times the scale (side_scale), times the class weight
+    float w = 0.f;
+    if (W > 0) {
+      float ff = 1.0f / (float)W;
+      ff *= sf;
+      w = wp * ff;
+    }
+    const bool good = !act || (nwo == 0 && nwf == W && shf == shf0 && mf && isfinite(w));
+    if (__ballot(!good) != 0) return false;
+    if (W == 0) return true;  // no sub-windows on any pass: the row adds nothing
+    // per-pass sources in lane k: receiver slice and table slice of sub-window 0, factor
+    const uint64_t rp = reinterpret_cast<uint64_t>(A.win + (int64_t)p * A.pass_stride + (int64_t)ch * A.ch_stride + a);
+    const uint64_t pp = reinterpret_cast<uint64_t>(tab_slice(tab, p, shf ? 0 : 2, 0));
+    const uint32_t rlo = (uint32_t)rp, rhi = (uint32_t)(rp >> 32), plo = (uint32_t)pp, phi = (uint32_t)(pp >> 32);
+    const uint32_t wv = __builtin_bit_cast(uint32_t, w);
+    // halves in order: pass k, sub-window s (cursor of the next half to hand out)
+    int hk = 0, hs = 0;
+    auto take = [&](const float*& r, const float2*& P, float& wt) {
+      const int k = hk;
+      r = reinterpret_cast<const float*>(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rhi, k) << 32) |
+                                         (uint32_t)__builtin_amdgcn_readlane((int)rlo, k)) + hs * A.hop;
+      P = reinterpret_cast<const float2*>(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)phi, k) << 32) |
+                                          (uint32_t)__builtin_amdgcn_readlane((int)plo, k)) + hs * kTabBins;
+      wt = __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)wv, k));
+      if (++hs == W) {
+        hs = 0;
+        ++hk;
+      }
+    };
+    const int M = W * n, nj = (M + 1) >> 1;
+    float2 U[NH];
+#pragma unroll
+    for (int j = 0; j < NH; ++j) U[j] = make_float2(0.f, 0.f);
+    const float *ra, *rb;
+    const float2 *Pa, *Pb;
+    float wa, wb = 0.f;
+    take(ra, Pa, wa);
+    bool hb = hk < n;
+    if (hb) take(rb, Pb, wb);
+    else {
+      rb = ra;
+      Pb = Pa;
+    }
+    float2 z[8];
+    load_ri(ra, rb, z);
+    for (int jb = 0; jb < nj; ++jb) {
+      uint32_t bp = 0, br = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bp |= nzbits(z[j].x);
+        br |= nzbits(z[j].y);
+      }
+      // a receiver slice or its pivot slice identically zero: exactly zero in the reference
+      const bool la = (__ballot(bp != 0) != 0) && sld(&Pa[kTabBins - 1].x) != 0.f;
+      const bool lb = hb && (__ballot(br != 0) != 0) && sld(&Pb[kTabBins - 1].x) != 0.f;
+      const bool live = la || lb;
+      if (live) stage1(z);
+      const float2 *Pa_c = Pa, *Pb_c = Pb;
+      const float wa_c = wa, wb_c = wb;
+      if (jb + 1 < nj) {  // the next pair's samples, loaded under this transform
+        take(ra, Pa, wa);
+        hb = hk < n;
+        if (hb) take(rb, Pb, wb);
+        else {
+          rb = ra;
+          Pb = Pa;
+        }
+        load_ri(ra, rb, z);
+      }
+      if (!live) continue;
+      float2 pa[NH], pb[NH];
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        const int f = max(bin(lane, j), 0);
+        pa[j] = Pa_c[f];
+        pb[j] = Pb_c[f];
+      }
+      finish_with([&](int j, float2 za, float2 zc) {
+        // z = R_a + i R_b: R_a = (Z[f] + conj Z[-f]) / 2, R_b = (Z[f] - conj Z[-f]) / 2i; w P conj(R)
+        if (la) {
+          const float2 r = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y - zc.y));
+          U[j].x += wa_c * (pa[j].x * r.x + pa[j].y * r.y);
+          U[j].y += wa_c * (pa[j].y * r.x - pa[j].x * r.y);
+        }
+        if (lb) {
+          const float2 r = make_float2(0.5f * (za.y + zc.y), -0.5f * (za.x - zc.x));
+          U[j].x += wb_c * (pb[j].x * r.x + pb[j].y * r.y);
+          U[j].y += wb_c * (pb[j].y * r.x - pb[j].x * r.y);
+        }
+      });
+    }
+    // Gh = (-1)^lane (conj on the shared window) U conj(tw[f])
+    const float sg = (lane & 1) ? -1.f : 1.f;
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      const int f = bin(lane, j);
+      if (f >= 0) {
+        const float2 t = tw[f];
+        const float2 x = cmul(shf0 ? make_float2(U[j].x, -U[j].y) : U[j], make_float2(t.x, -t.y));
+        Gh[j].x += sg * x.x;
+        Gh[j].y += sg * x.y;
+      }
+    }
+    return true;
   }
 
   __device__ const float2* inverse(const float2 (&Cf)[NH], const float2 (&Co)[NH]) {

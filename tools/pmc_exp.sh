@@ -27,3 +27,4 @@ json.dump(res, open(d + ".json", "w"), indent=1)
 for k, cs in res.items():
     print(k, " ".join("%s=%.4g" % (c, v) for c, v in sorted(cs.items())))
 PY
+rm -rf "$d"
