@@ -281,6 +281,10 @@ __device__ __forceinline__ const int32_t* tab_head(const float2* tab, int n_pass
 // their receivers, packed two per transform (z = R_a + i R_b, separated in stage 4 and multiplied into
 // the table's P conj(R)); the others keep z = P + i R.  On the configs[2] geometry that is 2 transforms
 // for a row whose only side is shared and 3 for a far row with both sides, against 3 and 6.
+#ifndef DVH_S1_SWIZZLE
+#define DVH_S1_SWIZZLE 1
+#endif
+
 struct EngF500 {
   static constexpr int N = 500;
   static constexpr int NFFT = 500;
@@ -337,8 +341,19 @@ struct EngF500 {
       if (r == 0 || i < 125) {
         float2 a[4] = {z[4 * r], z[4 * r + 1], z[4 * r + 2], z[4 * r + 3]};
         Dft<4>::run(a);
+#if DVH_S1_SWIZZLE
+        // the four outputs are two 16-byte stores, X[4i..4i+1] and X[4i+2..4i+3]; with both in that order an
+        // 8-lane store group hits banks 8i mod 32 twice (2-way conflict, the engine's only one).  Lanes with
+        // i & 4 store their second pair first, so each store's eight 16-byte pieces tile the 32 banks.
+        const bool sw = (lane & 4) != 0;
+        const int o = sw ? 2 : 0;
+        float4* d = reinterpret_cast<float4*>(bufB + 4 * i);
+        d[o >> 1] = sw ? make_float4(a[2].x, a[2].y, a[3].x, a[3].y) : make_float4(a[0].x, a[0].y, a[1].x, a[1].y);
+        d[(2 - o) >> 1] = sw ? make_float4(a[0].x, a[0].y, a[1].x, a[1].y) : make_float4(a[2].x, a[2].y, a[3].x, a[3].y);
+#else
 #pragma unroll
         for (int q = 0; q < 4; ++q) bufB[4 * i + q] = a[q];
+#endif
       }
     }
   }
