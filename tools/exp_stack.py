@@ -1,11 +1,11 @@
-"""Stack-launch breakdown on one synth10k batch (BASELINE configs[2] geometry), HIP-event timed:
+"""Stack-launch breakdown on one batch of a bench workload (default synth10k, BASELINE configs[2]), HIP-event timed:
 
     fused      vsg_stack_validated (correlation + whole-window scan in one launch, the bench's kernel)
     corr7      the same launch with a one-window scan: the correlation alone in the fused launch's layout
     corr       vsg_stack (the correlation alone, 4 waves per block)
     sumsq      window_sumsq of the batch (the validity as its own streaming pass)
 
-    python tools/exp_stack.py [--reps 20] [--only fused,corr]
+    python tools/exp_stack.py [--reps 20] [--only fused,corr] [--workload synth10k|weights|speeds]
 """
 import argparse
 import json
@@ -37,12 +37,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="fused,corr7,corr,sumsq")
+    ap.add_argument("--workload", default="synth10k", choices=("synth10k", "weights", "speeds"))
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    job = bench.build("synth10k", dev, 1, 0)
+    job = bench.build(args.workload, dev, 1, 0)
     b = job.batches[0]
-    job.plan_all.derive()
+    if getattr(job, "plan_all", None) is not None:
+        job.plan_all.derive()
+    elif b.derive:
+        b.plan.derive()
     vsg_scales(b.win, b.plan, out=b.scales, win_sumsq=None, validity=False)
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
