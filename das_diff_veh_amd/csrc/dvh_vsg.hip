@@ -585,8 +585,9 @@ __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2*
         float2 p0 = make_float2(0.f, 0.f), p1 = p0;
         if (X && f <= 250) {
           const float2 za = X[f], zc = X[f == 0 ? 0 : 500 - f];
-          p0 = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y - zc.y));
-          p1 = make_float2(0.5f * (za.y + zc.y), -0.5f * (za.x - zc.x));
+          // P / 2 of each slice (the consumers separate 2 R from their own transforms)
+          p0 = make_float2(0.25f * (za.x + zc.x), 0.25f * (za.y - zc.y));
+          p1 = make_float2(0.25f * (za.y + zc.y), -0.25f * (za.x - zc.x));
         }
         if (f == kTabBins - 1) {
           p0 = make_float2(l0 ? 1.f : 0.f, 0.f);

@@ -254,7 +254,8 @@ struct EngStockham {
 //   of the first gather row (the far rows' clamped windows).
 // A row side whose (start, nwin) equals its entry's transforms only its receivers, two per complex FFT.
 constexpr int kTabEnt = 4;
-constexpr int kTabBins = 256;  // bins f <= 250; [255].x = 1 when the slice has a non-zero sample
+constexpr int kTabBins = 256;  // bins f <= 250 (P / 2: the halving of z's separation folded in, exact);
+                                // [255].x = 1 when the slice has a non-zero sample
 constexpr int64_t kTabPassF2 = (int64_t)kTabEnt * 3 * kTabBins;  // float2 per pass
 
 __device__ __forceinline__ const float2* tab_slice(const float2* tab, int p, int e, int q) {
@@ -541,14 +542,14 @@ struct EngF500 {
         finish_with([&](int j, float2 za, float2 zc) {
           // z = R_a + i R_b: R_a = (Z[f] + conj Z[-f]) / 2, R_b = (Z[f] - conj Z[-f]) / 2i; P conj(R)
           if (la) {
-            const float2 r = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y - zc.y));
+            const float2 r = make_float2(za.x + zc.x, za.y - zc.y);  // 2 R_a (the table holds P / 2)
             const float2 c = make_float2(pa[j].x * r.x + pa[j].y * r.y, pa[j].y * r.x - pa[j].x * r.y);
             float2& C = fa ? Cf[j] : Co[j];
             C.x += c.x;
             C.y += c.y;
           }
           if (lb) {
-            const float2 r = make_float2(0.5f * (za.y + zc.y), -0.5f * (za.x - zc.x));
+            const float2 r = make_float2(za.y + zc.y, zc.x - za.x);  // 2 R_b
             const float2 c = make_float2(pb[j].x * r.x + pb[j].y * r.y, pb[j].y * r.x - pb[j].x * r.y);
             float2& C = fb ? Cf[j] : Co[j];
             C.x += c.x;
@@ -682,12 +683,12 @@ struct EngF500 {
       finish_with([&](int j, float2 za, float2 zc) {
         // z = R_a + i R_b: R_a = (Z[f] + conj Z[-f]) / 2, R_b = (Z[f] - conj Z[-f]) / 2i; w P conj(R)
         if (la) {
-          const float2 r = make_float2(0.5f * (za.x + zc.x), 0.5f * (za.y - zc.y));
+          const float2 r = make_float2(za.x + zc.x, za.y - zc.y);  // 2 R_a (the table holds P / 2)
           U[j].x += wa_c * (pa[j].x * r.x + pa[j].y * r.y);
           U[j].y += wa_c * (pa[j].y * r.x - pa[j].x * r.y);
         }
         if (lb) {
-          const float2 r = make_float2(0.5f * (za.y + zc.y), -0.5f * (za.x - zc.x));
+          const float2 r = make_float2(za.y + zc.y, zc.x - za.x);  // 2 R_b
           U[j].x += wb_c * (pb[j].x * r.x + pb[j].y * r.y);
           U[j].y += wb_c * (pb[j].y * r.x - pb[j].x * r.y);
         }
