@@ -180,3 +180,24 @@ def test_validated_stack_receiver_slices(batch, refs):
                 assert gio.gather_rel_err(got[s], ref) < TOL, (bad, s)
             else:
                 assert not np.isnan(got[s]).all(), (bad, s)
+
+
+def test_stack_mixed_chunks(batch, refs):
+    """Row tasks whose passes differ -- a regular pass with the two edge passes (one side's pivot slice
+    empty or shorter than a sub-window) in one chunk -- take the per-pass path where the cross-pass packing
+    (EngF500::direct_task) does not apply and the packed path where it does; the class means equal the
+    oracle's on every row the reference keeps finite (the edge passes' x / 0 rows are checked per pass in
+    test_edge_passes_inf_rows), and the regular class everywhere."""
+    from das_diff_veh_amd.vsg import StackSchedule, vsg_stack
+    from oracle import vsg as ovsg
+    slots = np.array([0, 1, 1, 1, 0, 0])
+    with np.errstate(all="ignore"):
+        ref1 = ovsg.stack([refs[i] for i in (1, 2, 3)])
+        ref0 = ovsg.stack([refs[i] for i in (0, 4, 5)])
+    rows = np.isfinite(ref0).all(axis=1)
+    assert rows.sum() > 100
+    for chunk in (3, 2):
+        got = vsg_stack(batch["win"], batch["plan"], StackSchedule(slots, 2, chunk=chunk),
+                        win_sumsq=batch["sumsq"]).double().cpu().numpy()
+        assert gio.gather_rel_err(got[1], ref1) < TOL, chunk
+        assert gio.gather_rel_err(got[0][rows], ref0[rows]) < TOL, chunk
