@@ -183,21 +183,22 @@ def test_validated_stack_receiver_slices(batch, refs):
 
 
 def test_stack_mixed_chunks(batch, refs):
-    """Row tasks whose passes differ -- a regular pass with the two edge passes (one side's pivot slice
-    empty or shorter than a sub-window) in one chunk -- take the per-pass path where the cross-pass packing
-    (EngF500::direct_task) does not apply and the packed path where it does; the class means equal the
-    oracle's on every row the reference keeps finite (the edge passes' x / 0 rows are checked per pass in
-    test_edge_passes_inf_rows), and the regular class everywhere."""
+    """Row tasks whose passes differ -- a regular pass with an edge pass (one side's pivot slice empty, so
+    that side is 0 / 0 and not averaged) in one chunk -- take the per-pass path where the cross-pass packing
+    (EngF500::direct_task) does not apply and the packed path where it does; both class means equal the
+    oracle's.  (The other edge pass, whose rows are x / 0, is parked in a third slot.)"""
     from das_diff_veh_amd.vsg import StackSchedule, vsg_stack
     from oracle import vsg as ovsg
-    slots = np.array([0, 1, 1, 1, 0, 0])
+    fin = [i for i in range(N_REG, N) if np.isfinite(refs[i]).all()]
+    assert fin
+    e = fin[0]
+    slots = np.array([0, 1, 1, 1, 2, 2])
+    slots[e] = 0
     with np.errstate(all="ignore"):
         ref1 = ovsg.stack([refs[i] for i in (1, 2, 3)])
-        ref0 = ovsg.stack([refs[i] for i in (0, 4, 5)])
-    rows = np.isfinite(ref0).all(axis=1)
-    assert rows.sum() > 100
+        ref0 = ovsg.stack([refs[i] for i in (0, e)])
     for chunk in (3, 2):
-        got = vsg_stack(batch["win"], batch["plan"], StackSchedule(slots, 2, chunk=chunk),
+        got = vsg_stack(batch["win"], batch["plan"], StackSchedule(slots, 3, chunk=chunk),
                         win_sumsq=batch["sumsq"]).double().cpu().numpy()
         assert gio.gather_rel_err(got[1], ref1) < TOL, chunk
-        assert gio.gather_rel_err(got[0][rows], ref0[rows]) < TOL, chunk
+        assert gio.gather_rel_err(got[0], ref0) < TOL, chunk
