@@ -547,8 +547,9 @@ def cpu_baseline(job, budget_s=20.0, workers=None):
                 sample=f"all cores: {workers} single-threaded processes x {budget_s / 2:.0f} s over {host.shape[0]} "
                        f"saved windows, {sum(n for n, _ in res)} windows (VSG two-sided), f-v images at the 1-core "
                        f"cost / {workers}; 1 core: {n_win} windows ({per_window * 1e3:.1f} ms/window), {n_img} f-v "
-                       f"images ({per_image * 1e3:.1f} ms/image) -> {rate1:.2f} windows/s; "
-                       f"cpu={platform.processor() or platform.machine()}",
+                       f"images ({per_image * 1e3:.1f} ms/image) -> {rate1:.2f} windows/s; the port leaves out the "
+                       f"reference's per-__add__ deepcopy of the window (apis/virtual_shot_gather.py:196), so the "
+                       f"reference itself is slower; cpu={platform.processor() or platform.machine()}",
                 value_1core=rate1)
 
 
@@ -615,7 +616,8 @@ def cpu_baseline_sliding(job, budget_s=20.0, workers=None):
                        f"{sum(n for n, _ in res)} (pass, pivot) units of 2 saved 4,096 x 8,192 windows (VSG two-sided, "
                        f"+-{half:.0f} m at each unit's pivot); {upp:.2f} units per pass; f-v images at the 1-core cost / "
                        f"{len(res)}; 1 core: {n_u} units ({per_unit * 1e3:.0f} ms/unit, the window's data / ||data|| "
-                       f"included), f-v image {per_image * 1e3:.1f} ms -> {rate1:.3f} passes/s; "
+                       f"included), f-v image {per_image * 1e3:.1f} ms -> {rate1:.3f} passes/s; without the "
+                       f"reference's per-__add__ deepcopy (apis/virtual_shot_gather.py:196); "
                        f"cpu={platform.processor() or platform.machine()}",
                 value_1core=rate1)
 
