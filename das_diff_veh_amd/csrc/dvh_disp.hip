@@ -760,9 +760,6 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 // bit-identical to what the other kernels compute.  (Forming the weights in the kernel from the query and
 // LDS tables of the k grid and fw measured slower: 1 207 vs 704 us for one image per wave, the LDS
 // bandwidth of the extra reads.)  Two images per wave (GI = 2) measured 673 vs 724 us for one.
-#ifndef DVH_FV_PAIR_STORE
-#define DVH_FV_PAIR_STORE 0  // 1: output tiles stored in pairs (under measurement)
-#endif
 #ifndef DVH_FV_MF_GI
 #define DVH_FV_MF_GI 2  // images per wave in lock step (1 or 2)
 #endif
@@ -944,11 +941,6 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
     // regular tiles t = 1 .. t_reg - 1, four per iteration so that the ring slots are static.  Tile t
     // consumes steps 4 t .. 4 t + 9; during it, steps 4 t + 10 .. 4 t + 13 are finished from pd (loaded
     // during tile t - 1) and steps 4 t + 14 .. 4 t + 17 are loaded into pd.
-#if DVH_FV_PAIR_STORE
-    // tiles stored in pairs: a row's 128-byte line gets both of its 64-byte halves from back-to-back stores
-    doublex4 pacc[GI];
-    int pt = -1;
-#endif
     for (int t0 = 1; t0 < t_reg; t0 += 4) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -973,19 +965,7 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
             acc[g] = mfma_f64(x[(4 * (u + 1) + s) & 15][g], bs, acc[g]);
           }
         }
-#if DVH_FV_PAIR_STORE
-        if (pt < 0) {
-#pragma unroll
-          for (int g = 0; g < GI; ++g) pacc[g] = acc[g];
-          pt = t;
-        } else {
-          store(pacc, kMfV * pt, fl_);
-          store(acc, kMfV * t, fl_);
-          pt = -1;
-        }
-#else
         store(acc, kMfV * t, fl_);
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) pd[i] = nx[i];
         // one tile per scheduling region, its samples finished in it
@@ -994,9 +974,6 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-#if DVH_FV_PAIR_STORE
-    if (pt >= 0) store(pacc, kMfV * pt, fl_);
-#endif
     launder();
     {  // last tile: rows nF - 16 .. nF - 1 (right fit), fresh samples in two groups of 5
       doublex4 acc[GI];
