@@ -59,7 +59,7 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="synth10k",
-                    choices=("synth10k", "weights", "speeds", "sliding", "timelapse"))
+                    choices=("synth10k", "weights", "speeds", "sliding", "timelapse", "bootstrap", "prep"))
     ap.add_argument("--scaling", default=None, choices=("weak", "strong", "both"),
                     help="weak: every rank its own job; strong: one job split over the ranks; both (default for "
                          "N > 1): the weak line with the strong (fixed-job) measurement beside it")
@@ -82,28 +82,69 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(argv, n):
+def launch_ranks(argv, n, poll_s=0.2, grace_s=10.0):
     """`python bench.py --gpus N` without a launcher: start N rank processes of this script (one per GPU,
     RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1), relay rank 0's output and
-    return the worst exit status.  Runs before torch is imported: this process never initialises HIP,
-    and it starts children instead of replacing itself (no exec after a GPU was touched)."""
+    return 0 when every rank exits 0.  Runs before torch is imported: this process never initialises HIP,
+    and it starts children instead of replacing itself (no exec after a GPU was touched).
+
+    All ranks are polled: the first rank that exits non-zero ends the run -- the others (blocked in a
+    rendezvous or a collective waiting for it) are terminated, then killed after `grace_s` -- and its exit
+    code and stderr tail are printed, so a failing rank never leaves the launch waiting for the
+    process-group timeout."""
+    import tempfile
+    import time as _time
     port = str(_free_port())
-    procs = []
+    tmp = tempfile.mkdtemp(prefix="dvh_ranks_")
+    procs, errs = [], []
+    out0 = open(os.path.join(tmp, "rank0.out"), "w+")
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        # rank 0's stderr streams through (progress lines); the other ranks' go to files, tailed on failure
+        err = None if r == 0 else open(os.path.join(tmp, f"rank{r}.err"), "w+")
+        errs.append(err)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out0, _ = procs[0].communicate()
-    sys.stdout.write(out0.decode())
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL, stderr=err))
+    failed = None
+    while failed is None and any(p.returncode is None for p in procs):
+        for r, p in enumerate(procs):
+            if p.returncode is None and p.poll() is not None and p.returncode != 0:
+                failed = r
+                break
+        else:
+            _time.sleep(poll_s)
+    if failed is not None:
+        for p in procs:
+            if p.returncode is None:
+                p.terminate()
+        t_end = _time.time() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - _time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    out0.seek(0)
+    sys.stdout.write(out0.read())
     sys.stdout.flush()
-    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
-    bad = [rc for rc in rcs if rc != 0]
-    if bad:
-        print(f"[bench] rank exit codes {rcs}", file=sys.stderr, flush=True)
-        return bad[0] if bad[0] > 0 else 1
-    return 0
+    rcs = [p.returncode for p in procs]
+    rc = 0
+    if failed is not None:
+        rc = procs[failed].returncode
+        tail = ""
+        if errs[failed] is not None:
+            errs[failed].seek(0)
+            tail = "".join(errs[failed].read().splitlines(True)[-20:])
+        print(f"[bench] rank {failed} exited with {rc}; the other ranks were stopped (exit codes {rcs})\n{tail}",
+              file=sys.stderr, flush=True)
+        rc = rc if rc > 0 else 1
+    for f in [out0] + [e for e in errs if e is not None]:
+        f.close()
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+    return rc
 
 
 if __name__ == "__main__":
@@ -115,6 +156,15 @@ if __name__ == "__main__":
               file=sys.stderr, flush=True)
         sys.exit(2)
     if _ARGS.launch_dry_run:
+        # test hook (tests/test_bench_launch.py): DVH_DRY_FAIL="rank:code" makes that rank exit with the code
+        # while every other rank blocks, as ranks waiting in a collective for a dead peer do
+        fail = os.environ.get("DVH_DRY_FAIL")
+        if fail:
+            fr, fc = (int(v) for v in fail.split(":"))
+            if int(os.environ["RANK"]) == fr:
+                print(f"[dry-run] rank {fr} fails with {fc}", file=sys.stderr, flush=True)
+                sys.exit(fc)
+            time.sleep(600)
         print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
                                                              "MASTER_PORT")}), flush=True)
         sys.exit(0)
@@ -156,6 +206,15 @@ WORKLOADS = {
                            "1-25 Hz, 200-1200 m/s) of 512 gathers of 25 ch x 500 lags per step and rank (a day's "
                            "stacks at 512 pivots): time DFT + channel contraction on the fp64 MFMA pipe, FITPACK "
                            "bilinear + Savitzky-Golay (fp64 MFMA); every rank images its own days"),
+    "bootstrap": dict(kind="bootstrap", config="SURVEY §8(f) row 1", n=1442, max_size=60, bt_times=30,
+                      desc="the notebooks' convergence_test (imaging_diff_speed.ipynb#cell30-31) for one class: 1,442 "
+                           "passes of 60 x 5,500 (pivot 700 m, 500-900 m), bt_size 1..60 x 30 resamples, 4 ridge modes "
+                           "(#cell25 sigma / ref_freq_idx / bands / reference curves); gathers from the resident "
+                           "windows, resample stacks, f-v images (242 x 1,000) and ridges every step"),
+    "prep": dict(kind="prep", config="SURVEY §8(f) row 2", n_ch=1024, seconds=60.0, dt=0.004,
+                 desc="TimeLapseImaging._preprocessing_for_surface_waves (apis/timeLapseImaging.py:51-71) of a "
+                      "continuous float32 record of 1,024 channels x 60 s at 250 Hz: bandpass_data (order-10 "
+                      "Butterworth 1.2-30 Hz, sosfiltfilt), empty / noisy trace imputation, per-trace L2 norm"),
     "sliding": dict(kind="sliding", config="configs[3]", n_total=12544, n_ch=4096, n_t=8192, pool=256, pivot_every=8,
                     half_aperture=200.0, gen_chunk=2, merge=49,
                     desc="configs[3]: synthetic passes x 4096 ch x 8192, sliding pivots every 8 channels (+-200 m, "
@@ -204,7 +263,12 @@ def build_pool(wl, device, world, rank, scaling, chunk):
     """configs[2]: a resident pool of windows, batches of `pool` passes with their own trajectories."""
     job = Job()
     pivot, start_x, end_x = wl["pivot"]
-    n_ch, n_t, pool = wl["n_ch"], wl["n_t"], wl["pool"]
+    n_ch, n_t = wl["n_ch"], wl["n_t"]
+    # the job's passes of this rank (below) cut into equal batches of at most ~1.05 x the nominal pool, so that no
+    # launch carries a remainder of a few passes (strong scaling: 5 120 per rank at N = 2 -> 10 x 512)
+    n_loc_pre = wl["n_total"] if scaling != "strong" else shard_passes(np.zeros(wl["n_total"], np.int64), world, rank).size
+    n_bat = max(1, -(-n_loc_pre // int(wl["pool"] * 1.05)))
+    pool = -(-n_loc_pre // n_bat) if n_loc_pre else wl["pool"]
     t0 = time.time()
     job.windows, x_axis, t_axis, _, _ = synth_batch_device(pool, n_ch=n_ch, n_t=n_t, pivot=pivot, seed=1000 * rank + 3,
                                                            device=device, x_first=wl["x_first"], track_half=10,
@@ -228,6 +292,7 @@ def build_pool(wl, device, world, rank, scaling, chunk):
     t0 = time.time()
     prm = VsgParams(pivot=pivot, start_x=start_x, end_x=end_x, wlen=2, norm=False, include_other_side=True)
     n_loc = mine.size
+    assert n_loc == n_loc_pre, (n_loc, n_loc_pre)
     trk_t = torch.empty((n_loc, xs.size), dtype=torch.float64, device=device)
     for b in range(0, n_loc, 1024):  # trajectories to the device in slices (bounded host memory)
         idx = mine[b:b + 1024]
@@ -385,6 +450,7 @@ def build_sliding(wl, device, world, rank, scaling, chunk):
         b.scan = UnitScan(np.tile(np.arange(pool) * n_ch, len(grp)),
                           np.concatenate([p.unit_window + k * pool for k, p in enumerate(grp)]), n_ch)
         b.scan_bytes = 4 * b.scan.n_win * n_ch * n_t
+        b.slots, b.first_batch, b.n_merged = sl, m0, len(grp)
         job.batches.append(b)
     job.units = sum(p.n_pass for p in plans)
     job.n_local = n_batch * pool
@@ -393,6 +459,7 @@ def build_sliding(wl, device, world, rank, scaling, chunk):
     job.cpu_sets = None
     job.cpu_units = dict(x_axis=x_axis, t_axis=t_axis, pch=pch, trk=trks[0], plan=plans[0],
                          half=wl["half_aperture"], units_per_pass=job.units / job.n_local)
+    job.plans, job.trks = plans, trks  # per batch of trajectories (host bookkeeping; tests/test_bench_job_gpu.py)
     R, w = plans[0].R, plans[0].w
     pv, st, en, _ = sliding_pivots(x_axis, pch[:1], wl["half_aperture"])
     job.finish(n_slot, R, w, x_axis[st[0]:en[0]] - x_axis[pv[0]], t_axis[1] - t_axis[0], device)
@@ -780,25 +847,264 @@ def timelapse_main(args, world, rank, device):
         dist.destroy_process_group()
 
 
+FP64_VALU_SPEC_TF = 78.6  # MI355X spec sheet, FP64 vector
+
+
+def prep_main(args, world, rank, device):
+    """one step = _preprocessing_for_surface_waves of a resident continuous record (a new
+    tensor each step, as the reference's data.copy()).  Records shard over the ranks (no exchange).
+    Roofline of the dominant kernels (dvh_sosfiltfilt's block filters): the sequential sosfiltfilt's
+    float64 operations (9 per sample per section, forward and backward over the padded extension) / the
+    bandpass' HIP-event time, against the FP64 vector peak; the block-parallel form issues 2x that."""
+    from das_diff_veh_amd.preprocess import _design, surface_wave_preprocessing
+    wl = WORKLOADS["prep"]
+    n_ch, dt = wl["n_ch"], wl["dt"]
+    n_t = int(round(wl["seconds"] / dt))
+    gen = torch.Generator(device=device)
+    gen.manual_seed(77 + rank)
+    t = torch.arange(n_t, device=device, dtype=torch.float64) * dt
+    rec = (torch.randn((n_ch, n_t), generator=gen, device=device, dtype=torch.float32) * 0.1 +
+           torch.sin(2 * np.pi * 7.0 * t)[None, :].float())
+    rec[100].zero_()          # an empty trace (imputed from its neighbours)
+    rec[333, 5000] = 1e3      # a noisy trace
+    sos, padlen, _, _ = _design(dt, 1.2, 30, device)
+    n_sec, n_ext = len(sos), n_t + 2 * padlen
+    phases = {}
+
+    def run(ph=None):
+        return surface_wave_preprocessing(rec, dt, _phases=ph)
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    evs = [{} for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        out = run(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = max_over_ranks(elapsed, device)
+    bp = float(np.mean([e["bandpass0"].elapsed_time(e["bandpass1"]) for e in evs])) / 1e3
+    cl = float(np.mean([e["bandpass1"].elapsed_time(e["cleanup1"]) for e in evs])) / 1e3
+    flop = 2.0 * 9 * n_sec * n_ext * n_ch  # sequential sosfiltfilt: forward + backward passes
+    rec_bytes = 4.0 * n_ch * n_t
+    # parity of the step's output against the oracle on a slice of traces (after timing)
+    from oracle import preprocess as oprep
+    host = rec.double().cpu().numpy()
+    ref = oprep.surface_wave_prep(host.astype(np.float32), dt)
+    got = out.double().cpu().numpy()
+    err = float(np.abs(got - ref).max() / np.abs(ref).max())
+    res = {
+        "metric": "continuous-record preprocessing: records/s (_preprocessing_for_surface_waves, 1,024 ch x 60 s); "
+                  "% FP64 roofline of the bandpass",
+        "value": world * args.steps / elapsed, "unit": "records/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64 recursion, f32 record",
+        "data": "synthetic float32 record (7 Hz tone + noise, one empty and one spiky trace), resident",
+        "config": {"workload": "prep", "baseline_config": wl["config"], "description": wl["desc"], "n_ch": n_ch,
+                   "n_t": n_t, "sections": n_sec, "padlen": padlen, "parallelism": f"dp{world} (records sharded)"},
+        "trace_samples_per_s": world * args.steps * n_ch * n_t / elapsed,
+        "roofline": {"bound": "fp64-valu", "achieved": flop / bp / 1e12, "peak": FP64_VALU_SPEC_TF, "unit": "TFLOP/s",
+                     "frac": flop / bp / 1e12 / FP64_VALU_SPEC_TF, "traffic": None,
+                     "kernel": "sos_block_kernel (dvh_sosfiltfilt: transition, 2 x (zero-state blocks, state scan, "
+                               "re-filter))",
+                     "launch_ms": bp * 1e3, "flop_model": "9 flops per sample per section (scipy sosfilt), forward + "
+                                                          "backward over n_t + 2 padlen; the block form issues 2x",
+                     "hbm_bytes_model": "record read + y (f64) written and read + record written",
+                     "hbm_frac": (2 * rec_bytes + 16.0 * n_ch * n_ext) / bp / 1e9 / HBM_PEAK_GBS},
+        "kernels_ms": {"bandpass": bp * 1e3, "trace_cleanup": cl * 1e3},
+        "parity": {"max_rel_err": err, "tol": 2e-6, "reference": "oracle/preprocess.py surface_wave_prep (float32 "
+                                                                  "record, scipy sosfiltfilt)"},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the oracle (scipy's sosfiltfilt + the reference's imputation / norm) on one core, on trace slices of the
+        # same record for ~cpu_budget / 2 s, scaled to the full record
+        torch.set_num_threads(1)
+        sub = host[:128].astype(np.float32)
+        n, t_c = 0, time.time()
+        while time.time() - t_c < args.cpu_budget / 2:
+            oprep.surface_wave_prep(sub, dt)
+            n += 1
+        secs = (time.time() - t_c) / n
+        res["cpu_baseline"] = {"value": sub.shape[0] / n_ch / secs, "unit": "records/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/preprocess.py surface_wave_prep on 128 of the record's traces, {n} runs "
+                                         f"({secs * 1e3:.0f} ms each), scaled x {n_ch // 128} to the 1,024-trace record; "
+                                         f"cpu={platform.processor() or platform.machine()}"}
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bootstrap_main(args, world, rank, device):
+    """one step = the notebook's convergence_test for one class (gathers of the class's
+    resident windows, then bt_size 1..60 x 30 resamples through one dispersion batch and 4 ridges).  Classes
+    shard over the ranks (no exchange).  Roofline of the dominant kernel (the MFMA f-v kernel over the 1,800
+    resample images)."""
+    import random
+
+    from das_diff_veh_amd import bootstrap as bt
+    from das_diff_veh_amd.disp import _use_mfma
+    from das_diff_veh_amd.plan import pack_trajectories
+    import scipy.interpolate
+    wl = WORKLOADS["bootstrap"]
+    n, S, T = wl["n"], wl["max_size"], wl["bt_times"]
+    wins, x_axis, t_axis, trk, _ = synth_batch_device(n, pivot=700.0, seed=3 + 1000 * rank, device=device)
+    tx, tt, tl = pack_trajectories(trk, device)
+    sigma, ref_idx, lb, ub = [25, 50, 50, 50], [80, 130, 170, 170], [2.5, 10, 14, 16], [14, 15, 19, 20]
+    curves = [None,
+              scipy.interpolate.interp1d([10, 12, 13, 14, 15, 16], [530, 470, 450, 430, 410, 391]),
+              scipy.interpolate.interp1d([14, 15, 16, 17, 18, 19], [630, 583, 550, 520, 500, 490]),
+              scipy.interpolate.interp1d([16, 17, 18, 19, 20, 21], [745, 690, 657, 626, 600, 580])]
+
+    def run(seed, ph=None):
+        if ph is not None:
+            ph.setdefault("gather0", torch.cuda.Event(enable_timing=True)).record()
+        cache = bt.GatherCache.from_device(wins, x_axis, t_axis, tx, tt, tl, 700.0, 500.0, 900.0)
+        return cache, bt.convergence(cache, S, T, sigma, ref_idx, lb, ub, curves, rand=random.Random(seed), phases=ph)
+
+    for k in range(args.warmup):
+        run(k)
+    torch.cuda.synchronize()
+    evs = [{} for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        cache, std = run(100 + k, evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = max_over_ranks(elapsed, device)
+
+    def span(a, b):
+        return float(np.mean([e[a].elapsed_time(e[b]) for e in evs])) / 1e3
+    t_gather, t_sel, t_disp, t_ridge = span("gather0", "select0"), span("select0", "select1"), \
+        span("select1", "disp1"), span("disp1", "ridge1")
+    _, _, plan = cache.disp_plan()
+    B = S * T
+    mfma = _use_mfma(plan, B)
+    # the f-v launch alone (dominant kernel): time it on its stream after the timed steps, same batch
+    stacks = cache.resample_stacks(np.tile(np.arange(1, 31, dtype=np.int32), (B, 1)))
+    FK = bt.fk_grid(stacks, plan)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(2):
+        bt.fv_from_fk(FK, plan)
+    reps = 5
+    e0.record()
+    for _ in range(reps):
+        bt.fv_from_fk(FK, plan)
+    e1.record()
+    torch.cuda.synchronize()
+    t_fv = e0.elapsed_time(e1) / reps / 1e3
+    n_tiles = -(-(plan.nF - 16) // 16) + 1
+    mfma_flop = 2.0 * 16 * 16 * 40 * n_tiles * B * -(-plan.nV // 16)
+    achieved = (mfma_flop if mfma else 2.0 * 25 * B * plan.nV * plan.nF) / t_fv / 1e12
+    res = {
+        "metric": "bootstrap convergence_test: resamples/s (one class, bt_size 1..60 x 30, 4 ridge modes); % MFMA "
+                  "roofline of the f-v kernel",
+        "value": world * B * args.steps / elapsed, "unit": "resamples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32 gathers / stacks, f64 dispersion (MFMA), f32 images",
+        "data": "synthetic passes (device-generated moving-source wavefield), resident windows; draws from "
+                "random.Random(seed) exactly as the notebook's random.sample",
+        "config": {"workload": "bootstrap", "baseline_config": wl["config"], "description": wl["desc"], "passes": n,
+                   "resamples_per_step": B, "nV": plan.nV, "nF": plan.nF, "gather_rows_imaged": plan.nch,
+                   "parallelism": f"dp{world} (classes sharded)"},
+        "step_breakdown_ms": {"gathers": t_gather * 1e3, "resample_stacks": t_sel * 1e3, "dispersion": t_disp * 1e3,
+                              "ridges_and_host": t_ridge * 1e3},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_SPEC_TF, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_MFMA_SPEC_TF, "frac_of_measured_ceiling": achieved / FP64_MFMA_PEAK_TF,
+                     "traffic": None, "kernel": "fv_mfma_kernel" if mfma else "fv_kernel", "launch_ms": t_fv * 1e3,
+                     "flop_model": "10 v_mfma_f64_16x16x4_f64 per (16 v x 16 f) tile" if mfma else "25-tap FIR",
+                     "hbm_frac": 4.0 * B * plan.nV * plan.nF / t_fv / 1e9 / HBM_PEAK_GBS},
+        "std_sum_mode0_first_last": [float(std[0, 0]), float(std[0, -1])],
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the reference's bootstrap_disp recomputes every gather of every resample: its cost per resample of
+        # size k is k VSG gathers + one f-v image + 4 ridges; timed with the oracle on one core (gather, f-v
+        # image, ridge) on the bench's own windows, then priced over the step's 1,800 resamples
+        from oracle import ref_loop
+        from oracle import ridge as orid
+        torch.set_num_threads(1)
+        host = wins[:8].double().cpu().numpy()
+        tg, ng, t_c = 0.0, 0, time.time()
+        gs = []
+        while time.time() - t_c < args.cpu_budget / 3 or ng < 2:
+            i = ng % host.shape[0]
+            ta = time.time()
+            g, gx, gt = ref_loop.gather(host[i], x_axis, t_axis, trk[i][0], trk[i][1], 700.0, 500.0, 900.0)
+            tg += time.time() - ta
+            ng += 1
+            gs.append(g)
+        ta = time.time()
+        fv = ref_loop.disp_image(np.mean(gs, axis=0), gx, gt, start_x=-150, end_x=0)
+        t_img = time.time() - ta
+        ta = time.time()
+        fq = bt.FREQS
+        for m in range(4):
+            band = (fq >= lb[m]) & (fq < ub[m])
+            try:
+                orid.extract_ridge_ref_idx(fq[band], bt.VELS, fv[:, band], ref_freq_idx=ref_idx[m] - int(np.sum(fq < lb[m])),
+                                           sigma=sigma[m], vel_max=800, ref_vel=curves[m])
+            except ValueError:
+                pass
+        t_rdg = time.time() - ta
+        per_g = tg / ng
+        windows_drawn = T * S * (S + 1) // 2
+        cpu_s = windows_drawn * per_g + B * (t_img + t_rdg)
+        res["cpu_baseline"] = {"value": B / cpu_s, "unit": "resamples/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle on one core: {ng} VSG gathers ({per_g * 1e3:.1f} ms each, "
+                                         f"oracle/ref_loop.py), one f-v image ({t_img * 1e3:.1f} ms, map_fv) and 4 "
+                                         f"ridges ({t_rdg * 1e3:.1f} ms), priced over the step: {windows_drawn} gathers "
+                                         f"(the reference recomputes every resample's gathers) + {B} images + ridges; "
+                                         f"cpu={platform.processor() or platform.machine()}"}
+        res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = _ARGS
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    local %= max(1, torch.cuda.device_count())  # identity with one rank per GPU; several ranks share a GPU otherwise
+    backend = os.environ.get("DVH_DIST_BACKEND", "nccl")
+    n_dev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and local >= n_dev:
+        # one rank per GPU: fewer visible GPUs than local ranks is a launch error, never two ranks on one device
+        raise SystemExit(f"[bench] rank {rank}: LOCAL_RANK {local} but only {n_dev} visible GPU(s); RCCL runs one "
+                         f"rank per GPU (DVH_DIST_BACKEND=gloo rehearses several ranks on one GPU)")
+    if backend != "nccl":
+        local %= max(1, n_dev)  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         # RCCL over xGMI, one rank per GPU; DVH_DIST_BACKEND=gloo rehearses the multi-rank step with
         # several ranks on one GPU (RCCL refuses that), reducing through host copies
-        backend = os.environ.get("DVH_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"[bench] world size {dist.get_world_size()} != --gpus {args.gpus}")
 
-    if WORKLOADS[args.workload]["kind"] == "timelapse":
-        return timelapse_main(args, world, rank, device)
+    kind = WORKLOADS[args.workload]["kind"]
+    if kind in ("timelapse", "bootstrap", "prep"):
+        return {"timelapse": timelapse_main, "bootstrap": bootstrap_main, "prep": prep_main}[kind](args, world, rank,
+                                                                                                   device)
     if args.sliding_merge is not None:
         WORKLOADS["sliding"]["merge"] = args.sliding_merge
     scaling = args.scaling or ("weak" if world == 1 else "both")

@@ -163,13 +163,8 @@ def convergence_test(max_sample_num, windows, bt_times, sigma, x0, start_x, end_
                      vel_ref):
     """imaging_diff_speed.ipynb#cell30: for bt_size = 1..max_sample_num, the summed per-frequency
     std of the bootstrap ridges -> [n_modes, max_sample_num].  The gathers are computed once for all
-    60 x bt_times resamples (the notebook recomputes them per resample); draws as the notebook's."""
+    60 x bt_times resamples (the notebook recomputes them per resample); draws as the notebook's; all
+    resamples imaged in one batch (das_diff_veh_amd.bootstrap.convergence)."""
     from .. import bootstrap as bt
     cache = bt.GatherCache(windows, x0, start_x, end_x)
-    out = np.empty((len(freq_lb), max_sample_num))
-    for bt_size in range(1, max_sample_num + 1):
-        sels = bt.draw(len(windows), bt_size, bt_times)
-        per_mode = bt.bootstrap_ridges(cache, sels, sigma, ref_freq_idx, freq_lb, freq_ub, vel_ref)
-        for m, r in enumerate(per_mode):
-            out[m, bt_size - 1] = np.sum(np.std(r, axis=0))
-    return out
+    return bt.convergence(cache, max_sample_num, bt_times, sigma, ref_freq_idx, freq_lb, freq_ub, vel_ref)

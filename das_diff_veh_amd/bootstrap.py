@@ -107,6 +107,28 @@ class GatherCache:
         self.n = len(windows)
         self._disp = {}
 
+    @classmethod
+    def from_device(cls, data, x_axis, t_axis, trk_x, trk_t, trk_len, pivot, start_x, end_x, wlen=2,
+                    include_other_side=True):
+        """The cache of windows already resident as one float32 device tensor [n, C, T] on shared axes, with
+        the index tables derived on the device from packed trajectories (plan.pack_trajectories layout,
+        dvh_pass_geometry): no per-pass host work (the bench's bootstrap job)."""
+        from .plan import DevicePlan
+        self = cls.__new__(cls)
+        self.device = data.device
+        self.prm = VsgParams(pivot=pivot, start_x=start_x, end_x=end_x, wlen=wlen, norm=False,
+                             include_other_side=include_other_side)
+        self.plan = DevicePlan(x_axis, t_axis, trk_x, trk_t, trk_len, self.prm, data.shape[1])
+        self.G = vsg_gathers(data, self.plan)
+        x_axis, t_axis = np.asarray(x_axis, dtype=np.float64), np.asarray(t_axis, dtype=np.float64)
+        pv, st = int(np.argmax(x_axis >= pivot)), int(np.argmax(x_axis >= start_x))
+        dt = t_axis[1] - t_axis[0]
+        self.gx = x_axis[st:st + self.plan.R] - x_axis[pv]
+        self.gt = (np.arange(self.plan.w) - self.plan.w // 2) * dt
+        self.n = data.shape[0]
+        self._disp = {}
+        return self
+
     def disp_plan(self, start_x=-150, end_x=0, freqs=FREQS, vels=VELS):
         """compute_disp_image's nearest-offset channel slice and its DispPlan (dx = 8.16, :247-258)."""
         s = int(np.abs(self.gx - start_x).argmin())
@@ -117,15 +139,19 @@ class GatherCache:
             self._disp[key] = (s, e, DispPlan(e + 1 - s, self.plan.w, 8.16, dt, freqs, vels))
         return self._disp[key]
 
-    def resample_stacks(self, sel, start_x=-150, end_x=0):
-        """Mean gathers over the disp rows for every draw: sel [B, k] pass indices -> [B, nch, w]."""
+    def resample_stacks(self, sel, start_x=-150, end_x=0, out=None):
+        """Mean gathers over the disp rows for every draw: sel [B, k] pass indices -> [B, nch, w] (into
+        ``out``, a contiguous [B, nch, w] float32 device tensor, when given)."""
         sel = np.asarray(sel, dtype=np.int32)
         if sel.ndim != 2 or sel.size == 0 or sel.min() < 0 or sel.max() >= self.n:
             raise ValueError("selections must be [B, k] pass indices")
         s, e, _ = self.disp_plan(start_x, end_x)
         w, R = self.plan.w, self.plan.R
         B, k = sel.shape
-        out = torch.empty((B, e + 1 - s, w), dtype=torch.float32, device=self.device)
+        if out is None:
+            out = torch.empty((B, e + 1 - s, w), dtype=torch.float32, device=self.device)
+        elif tuple(out.shape) != (B, e + 1 - s, w) or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous float32 [{B}, {e + 1 - s}, {w}] tensor")
         sel_t = torch.as_tensor(sel, device=self.device)
         base = self.G[:, s:e + 1, :]
         _lib.call("dvh_select_mean", _lib.ptr(base), R * w, (e + 1 - s) * w, _lib.ptr(sel_t), B, k, _lib.ptr(out),
@@ -147,6 +173,38 @@ def bootstrap_ridges(cache: GatherCache, sels, sigma, ref_freq_idx, freq_lb, fre
         ref = ref_freq_idx[m] - int(np.sum(FREQS < freq_lb[m]))
         out.append(ridges(fv, FREQS, VELS, freq_lb[m], freq_up[m], ref_freq_idx=ref, sigma=sigma[m], vel_max=800,
                           ref_vel=ref_vel[m]))
+    return out
+
+
+def convergence(cache: GatherCache, max_size, bt_times, sigma, ref_freq_idx, freq_lb, freq_up, ref_vel, start_x=-150,
+                end_x=0, rand=random, phases=None):
+    """The notebooks' convergence_test (imaging_diff_speed.ipynb#cell30) on a gather cache: for bt_size =
+    1..max_size, bt_times resamples (the same random.sample draws in the same order as the notebook's
+    per-size bootstrap_disp calls), their ridges per mode, and the summed per-frequency std -> [n_modes,
+    max_size].  All max_size x bt_times resamples go through ONE dispersion batch (select_mean per size
+    into one buffer, one tdft / fk / f-v launch each, one ridge launch per mode), so the host synchronises
+    once per mode instead of once per (size, mode).  ``phases`` (optional dict) receives torch events
+    around the resample / dispersion / ridge parts for timing."""
+    sels = [draw(cache.n, k, bt_times, rand) for k in range(1, max_size + 1)]
+    s, e, plan = cache.disp_plan(start_x, end_x)
+    B = max_size * bt_times
+    ev = (lambda name: phases.setdefault(name, torch.cuda.Event(enable_timing=True)).record()) if phases is not None \
+        else (lambda name: None)
+    ev("select0")
+    stacks = torch.empty((B, e + 1 - s, plan.nt), dtype=torch.float32, device=cache.device)
+    for k, sel in enumerate(sels):
+        cache.resample_stacks(sel, start_x, end_x, out=stacks[k * bt_times:(k + 1) * bt_times])
+    ev("select1")
+    fv = fv_from_fk(fk_grid(stacks, plan), plan)
+    ev("disp1")
+    out = np.empty((len(freq_lb), max_size))
+    for m in range(len(freq_lb)):
+        ref = ref_freq_idx[m] - int(np.sum(FREQS < freq_lb[m]))
+        r = ridges(fv, FREQS, VELS, freq_lb[m], freq_up[m], ref_freq_idx=ref, sigma=sigma[m], vel_max=800,
+                   ref_vel=ref_vel[m])
+        for k in range(max_size):
+            out[m, k] = np.sum(np.std(r[k * bt_times:(k + 1) * bt_times], axis=0))
+    ev("ridge1")
     return out
 
 

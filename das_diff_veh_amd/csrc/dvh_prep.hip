@@ -2,8 +2,8 @@
 //
 //   dvh_sosfiltfilt  bandpass_data (modules/utils.py:179-189): scipy.signal.sosfiltfilt(sos, x, axis=1)
 //                    = odd extension by padlen, sosfilt with zi * x_ext[0], reverse, sosfilt with
-//                    zi * y[-1], reverse, trim.  One lane per trace, float64 recursion (the order-10
-//                    band edge at 1.2 Hz / 125 Hz puts poles within 1e-2 of the unit circle).
+//                    zi * y[-1], reverse, trim.  Float64 recursion, time-parallel over blocks of each
+//                    trace (zero-state block filters + a state scan + re-filter, below).
 //   dvh_mute_traj    SurfaceWaveWindow.mute_along_traj (apis/data_classes.py:49-72): column t is
 //                    multiplied by a tukey taper placed along the vehicle trajectory (host tables).
 //   dvh_mute_time    SurfaceWaveWindow.mute_along_time (apis/data_classes.py:100-104).
@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "dvh_common.h"
 #include "dvh.h"
 
@@ -22,64 +24,249 @@ namespace dvh {
 
 constexpr int kMaxSec = 16;
 
-template <typename T>
-__global__ __launch_bounds__(64) void sosfiltfilt_kernel(T* __restrict__ x, int64_t n_rows, int64_t row_stride,
-                                                          int32_t n_t, const double* __restrict__ sos,
-                                                          int32_t n_sec, int32_t padlen,
-                                                          const double* __restrict__ zi,
-                                                          double* __restrict__ work) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n_rows) return;
-  T* row = x + r * row_stride;
-  const int64_t n_ext = (int64_t)n_t + 2 * padlen;
-  double* y = work + r * n_ext;
-  double b0[kMaxSec], b1[kMaxSec], b2[kMaxSec], a1[kMaxSec], a2[kMaxSec], z0[kMaxSec], z1[kMaxSec];
-  for (int s = 0; s < n_sec; ++s) {
-    b0[s] = sos[6 * s];
-    b1[s] = sos[6 * s + 1];
-    b2[s] = sos[6 * s + 2];
-    a1[s] = sos[6 * s + 4];
-    a2[s] = sos[6 * s + 5];
+// ---------------------------------------------------------------------------------------------
+// sosfiltfilt, time-parallel.  The cascade of n_sec transposed-direct-form-II sections (scipy's sosfilt:
+// o = b0 v + z0; z0 = b1 v - a1 o + z1; z1 = b2 v - a2 o) is linear in its 2 n_sec states, so a sequence
+// u[0, n_ext) cut into blocks of L samples is filtered block-parallel in three phases:
+//   A  every block except the last is filtered from ZERO state (block 0 from the true initial state
+//      zi * u[0]), keeping only its end state e_k;
+//   B  per row, the true end states follow by a scan over the blocks, s_k = e_k + M s_{k-1} with
+//      M = A^L the zero-input state transition of L samples (sos_transition_kernel forms it on the
+//      device with the filter's own arithmetic);
+//   C  every block is filtered again from its true start state s_{k-1} and writes its outputs.
+// sosfiltfilt = the forward pass over the odd extension ext(x) (zi * ext[0]), then the backward pass over
+// the reversed forward output y (zi * y[-1]), trimmed by padlen.  One lane per (row, block): n_rows x n_ext
+// / L lanes instead of n_rows (a 1 024-trace record filled 16 of the chip's 1 024 SIMDs with one lane per
+// trace).  The poles of the order-10 band (1.2 Hz at fs = 250 Hz) sit about 1e-2 inside the unit circle,
+// so M is a contraction and the scan is well conditioned.
+template <int NS>
+struct SosCoef {
+  double b0[NS], b1[NS], b2[NS], a1[NS], a2[NS];
+  __device__ __forceinline__ void load(const double* __restrict__ sos) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      b0[s] = sos[6 * s];
+      b1[s] = sos[6 * s + 1];
+      b2[s] = sos[6 * s + 2];
+      a1[s] = sos[6 * s + 4];
+      a2[s] = sos[6 * s + 5];
+    }
   }
-  const double x0 = (double)row[0], xn = (double)row[n_t - 1];
-  // ext[i]: i < padlen -> 2 x0 - x[padlen - i]; i >= padlen + n_t -> 2 xn - x[n_t - 2 - (i - padlen - n_t)]
-  auto ext = [&](int64_t i) -> double {
+  // one sample through the cascade (scipy's sosfilt expressions)
+  __device__ __forceinline__ double step(double (&z0)[NS], double (&z1)[NS], double v) const {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const double o = b0[s] * v + z0[s];
+      z0[s] = b1[s] * v - a1[s] * o + z1[s];
+      z1[s] = b2[s] * v - a2[s] * o;
+      v = o;
+    }
+    return v;
+  }
+};
+
+// The filtered sequence u of a row: the odd extension of x (forward pass) or the reversed forward output.
+template <typename T, bool BWD>
+struct SosInput {
+  const T* row;      // forward: the row of x
+  const double* y;   // backward: the row's forward output [n_ext]
+  int64_t n_t, n_ext, padlen;
+  double x0, xn;
+  __device__ __forceinline__ double operator()(int64_t i) const {
+    if (BWD) return y[n_ext - 1 - i];
     if (i < padlen) return 2.0 * x0 - (double)row[padlen - i];
     const int64_t j = i - padlen;
     if (j < n_t) return (double)row[j];
     return 2.0 * xn - (double)row[n_t - 2 - (j - n_t)];
-  };
-  const double e0 = ext(0);
-  for (int s = 0; s < n_sec; ++s) {
-    z0[s] = zi[2 * s] * e0;
-    z1[s] = zi[2 * s + 1] * e0;
   }
-  for (int64_t i = 0; i < n_ext; ++i) {
-    double v = ext(i);
-    for (int s = 0; s < n_sec; ++s) {
-      const double o = b0[s] * v + z0[s];
-      z0[s] = b1[s] * v - a1[s] * o + z1[s];
-      z1[s] = b2[s] * v - a2[s] * o;
-      v = o;
+};
+
+struct SosGeom {
+  int64_t n_rows, row_stride;
+  int32_t n_t, padlen, L, nb;
+  int64_t n_ext;
+};
+
+template <typename T, bool BWD>
+__device__ __forceinline__ SosInput<T, BWD> sos_input(const T* x, const double* y, const SosGeom& G, int64_t r) {
+  SosInput<T, BWD> u;
+  u.row = x + r * G.row_stride;
+  u.y = y + r * G.n_ext;
+  u.n_t = G.n_t;
+  u.n_ext = G.n_ext;
+  u.padlen = G.padlen;
+  if (!BWD) {
+    u.x0 = (double)u.row[0];
+    u.xn = (double)u.row[G.n_t - 1];
+  } else {
+    u.x0 = u.xn = 0.0;
+  }
+  return u;
+}
+
+// M[j][m] (row-major, 2 NS states ordered z0[0], z1[0], z0[1], ...): the state after L zero-input samples
+// from the unit state e_m.  One wave, lane m < 2 NS.
+template <int NS>
+__global__ __launch_bounds__(64) void sos_transition_kernel(const double* __restrict__ sos, int32_t L,
+                                                             double* __restrict__ M) {
+  constexpr int NST = 2 * NS;
+  const int m = threadIdx.x;
+  if (m >= NST) return;
+  SosCoef<NS> c;
+  c.load(sos);
+  double z0[NS], z1[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    z0[s] = (2 * s == m) ? 1.0 : 0.0;
+    z1[s] = (2 * s + 1 == m) ? 1.0 : 0.0;
+  }
+  for (int i = 0; i < L; ++i) c.step(z0, z1, 0.0);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    M[(2 * s) * NST + m] = z0[s];
+    M[(2 * s + 1) * NST + m] = z1[s];
+  }
+}
+
+// Phases A (OUT = false: end states of blocks k < nb - 1 into S) and C (OUT = true: filter from the true start
+// state S[k - 1] and write the outputs: y[i] forward, the trimmed row backward).  Lane g = r * nb + k.
+template <typename T, int NS, bool BWD, bool OUT>
+__global__ __launch_bounds__(256) void sos_block_kernel(T* __restrict__ x, double* __restrict__ y, SosGeom G,
+                                                         const double* __restrict__ sos, const double* __restrict__ zi,
+                                                         double* __restrict__ S) {
+  constexpr int NST = 2 * NS;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G.n_rows * G.nb) return;
+  const int64_t r = g / G.nb;
+  const int k = (int)(g - r * G.nb);
+  if (!OUT && k == G.nb - 1) return;  // the last block's end state is not needed
+  const SosInput<T, BWD> u = sos_input<T, BWD>(x, y, G, r);
+  SosCoef<NS> c;
+  c.load(sos);
+  double z0[NS], z1[NS];
+  double* Sr = S + g * NST;  // S[r][k]
+  if (k == 0) {
+    const double u0 = u(0);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      z0[s] = zi[2 * s] * u0;
+      z1[s] = zi[2 * s + 1] * u0;
     }
-    y[i] = v;
-  }
-  const double yl = y[n_ext - 1];
-  for (int s = 0; s < n_sec; ++s) {
-    z0[s] = zi[2 * s] * yl;
-    z1[s] = zi[2 * s + 1] * yl;
-  }
-  for (int64_t i = n_ext - 1; i >= 0; --i) {
-    double v = y[i];
-    for (int s = 0; s < n_sec; ++s) {
-      const double o = b0[s] * v + z0[s];
-      z0[s] = b1[s] * v - a1[s] * o + z1[s];
-      z1[s] = b2[s] * v - a2[s] * o;
-      v = o;
+  } else if (OUT) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      z0[s] = Sr[-NST + 2 * s];
+      z1[s] = Sr[-NST + 2 * s + 1];
     }
-    y[i] = v;
+  } else {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) z0[s] = z1[s] = 0.0;
   }
-  for (int32_t t = 0; t < n_t; ++t) row[t] = (T)y[padlen + t];
+  const int64_t i0 = (int64_t)k * G.L, i1 = min(i0 + G.L, G.n_ext);
+  if (!OUT) {
+    for (int64_t i = i0; i < i1; ++i) c.step(z0, z1, u(i));
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      Sr[2 * s] = z0[s];
+      Sr[2 * s + 1] = z1[s];
+    }
+  } else if (!BWD) {
+    double* yr = y + r * G.n_ext;
+    for (int64_t i = i0; i < i1; ++i) yr[i] = c.step(z0, z1, u(i));
+  } else {
+    T* row = x + r * G.row_stride;
+    // reversed index i is sample n_ext - 1 - i of the extension; the row keeps [padlen, padlen + n_t)
+    for (int64_t i = i0; i < i1; ++i) {
+      const double v = c.step(z0, z1, u(i));
+      const int64_t j = G.n_ext - 1 - i - G.padlen;
+      if (j >= 0 && j < G.n_t) row[j] = (T)v;
+    }
+  }
+}
+
+// Phase B: s_k = e_k + M s_{k-1} for k = 1 .. nb - 2 (s_0 = e_0 is already the true state).  Two rows per
+// wave (lanes 0-31 / 32-63), lane j = state component j.
+template <int NS>
+__global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* __restrict__ M, double* __restrict__ S) {
+  constexpr int NST = 2 * NS;
+  const int half = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const int64_t r = 2 * (int64_t)blockIdx.x + half;
+  const bool act = r < G.n_rows && j < NST;
+  double m[NST];
+#pragma unroll
+  for (int i = 0; i < NST; ++i) m[i] = act ? M[j * NST + i] : 0.0;
+  double* Sr = S + (act ? r : 0) * (int64_t)G.nb * NST;
+  double s = act ? Sr[j] : 0.0;
+  const int base = half * 32;
+  for (int k = 1; k < G.nb - 1; ++k) {
+    double acc = act ? Sr[(int64_t)k * NST + j] : 0.0;
+#pragma unroll
+    for (int i = 0; i < NST; ++i) acc += m[i] * __shfl(s, base + i);
+    if (act) Sr[(int64_t)k * NST + j] = acc;
+    s = acc;
+  }
+}
+
+// block length: enough (row, block) lanes for ~4 waves per SIMD, blocks of 32 .. 4096 samples
+static int sos_block_len(int64_t n_rows, int64_t n_ext) {
+  const int64_t target = 256LL * 4 * 4 * 64;
+  int64_t L = (n_rows * n_ext + target - 1) / target;
+  L = (L + 31) / 32 * 32;
+  return (int)std::min<int64_t>(std::max<int64_t>(L, 32), 4096);
+}
+
+static SosGeom sos_geom(int64_t n_rows, int64_t row_stride, int32_t n_t, int32_t padlen) {
+  SosGeom G;
+  G.n_rows = n_rows;
+  G.row_stride = row_stride;
+  G.n_t = n_t;
+  G.padlen = padlen;
+  G.n_ext = (int64_t)n_t + 2 * padlen;
+  G.L = sos_block_len(n_rows, G.n_ext);
+  G.nb = (int32_t)((G.n_ext + G.L - 1) / G.L);
+  return G;
+}
+
+// workspace: y [n_rows][n_ext] + S [n_rows][nb][2 n_sec] + M [2 n_sec]^2, doubles
+static int64_t sos_workspace_doubles(const SosGeom& G, int n_sec) {
+  const int64_t nst = 2 * n_sec;
+  return G.n_rows * G.n_ext + G.n_rows * G.nb * nst + nst * nst;
+}
+
+template <typename T, int NS>
+static int sosfiltfilt_blocks(T* x, const SosGeom& G, const double* sos, const double* zi, double* work,
+                              hipStream_t st) {
+  constexpr int NST = 2 * NS;
+  double* y = work;
+  double* S = y + G.n_rows * G.n_ext;
+  double* M = S + G.n_rows * G.nb * NST;
+  const int64_t lanes = G.n_rows * G.nb;
+  const dim3 grid((unsigned)((lanes + 255) / 256)), scan_grid((unsigned)((G.n_rows + 1) / 2));
+  hipLaunchKernelGGL(sos_transition_kernel<NS>, dim3(1), dim3(64), 0, st, sos, G.L, M);
+  // forward pass over the odd extension -> y
+  hipLaunchKernelGGL((sos_block_kernel<T, NS, false, false>), grid, dim3(256), 0, st, x, y, G, sos, zi, S);
+  if (G.nb > 2) hipLaunchKernelGGL(sos_scan_kernel<NS>, scan_grid, dim3(64), 0, st, G, (const double*)M, S);
+  hipLaunchKernelGGL((sos_block_kernel<T, NS, false, true>), grid, dim3(256), 0, st, x, y, G, sos, zi, S);
+  // backward pass over reversed y -> the trimmed row
+  hipLaunchKernelGGL((sos_block_kernel<T, NS, true, false>), grid, dim3(256), 0, st, x, y, G, sos, zi, S);
+  if (G.nb > 2) hipLaunchKernelGGL(sos_scan_kernel<NS>, scan_grid, dim3(64), 0, st, G, (const double*)M, S);
+  hipLaunchKernelGGL((sos_block_kernel<T, NS, true, true>), grid, dim3(256), 0, st, x, y, G, sos, zi, S);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
+}
+
+template <typename T>
+static int sosfiltfilt_dispatch(T* x, const SosGeom& G, const double* sos, int n_sec, const double* zi, double* work,
+                                hipStream_t st) {
+  switch (n_sec) {
+#define DVH_SOS_CASE(n) \
+  case n: return sosfiltfilt_blocks<T, n>(x, G, sos, zi, work, st);
+    DVH_SOS_CASE(1) DVH_SOS_CASE(2) DVH_SOS_CASE(3) DVH_SOS_CASE(4) DVH_SOS_CASE(5) DVH_SOS_CASE(6)
+    DVH_SOS_CASE(7) DVH_SOS_CASE(8) DVH_SOS_CASE(9) DVH_SOS_CASE(10) DVH_SOS_CASE(11) DVH_SOS_CASE(12)
+    DVH_SOS_CASE(13) DVH_SOS_CASE(14) DVH_SOS_CASE(15) DVH_SOS_CASE(16)
+#undef DVH_SOS_CASE
+    default: return set_error(-4, "unsupported number of second-order sections");
+  }
 }
 
 // tab[(p * n_t + t) * 3 + {0,1,2}] = {start, end, taper_start}; element (x, t) of pass p is scaled by
@@ -270,6 +457,11 @@ DVH_API int dvh_trace_cleanup(void* x, int32_t dtype, int64_t n_rows, int64_t ro
   return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
 }
 
+DVH_API int64_t dvh_sosfiltfilt_workspace(int64_t n_rows, int32_t n_t, int32_t n_sec, int32_t padlen) {
+  if (n_rows <= 0 || n_t <= 0 || n_sec <= 0 || n_sec > kMaxSec || padlen < 0) return 0;
+  return 8 * sos_workspace_doubles(sos_geom(n_rows, n_t, n_t, padlen), n_sec);
+}
+
 DVH_API int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t,
                             const double* sos, int32_t n_sec, int32_t padlen, const double* zi, double* work,
                             void* stream) {
@@ -278,16 +470,10 @@ DVH_API int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_
   if (n_t <= padlen) return set_error(-4, "The length of the input vector x must be greater than padlen");
   if (padlen < 0 || n_t < 2) return set_error(-2, "invalid padlen / length");
   if (n_rows <= 0) return 0;
-  const dim3 grid((unsigned)((n_rows + 63) / 64));
-  if (dtype == 0)
-    hipLaunchKernelGGL(sosfiltfilt_kernel<float>, grid, dim3(64), 0, (hipStream_t)stream, (float*)x, n_rows,
-                       row_stride, n_t, sos, n_sec, padlen, zi, work);
-  else if (dtype == 1)
-    hipLaunchKernelGGL(sosfiltfilt_kernel<double>, grid, dim3(64), 0, (hipStream_t)stream, (double*)x, n_rows,
-                       row_stride, n_t, sos, n_sec, padlen, zi, work);
-  else
-    return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
-  return last_launch();
+  const SosGeom G = sos_geom(n_rows, row_stride, n_t, padlen);
+  if (dtype == 0) return sosfiltfilt_dispatch<float>((float*)x, G, sos, n_sec, zi, work, (hipStream_t)stream);
+  if (dtype == 1) return sosfiltfilt_dispatch<double>((double*)x, G, sos, n_sec, zi, work, (hipStream_t)stream);
+  return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
 }
 
 DVH_API int dvh_mute_traj(void* data, int32_t dtype, int32_t n_pass, int64_t pass_stride, int32_t n_ch, int32_t n_t,

@@ -65,7 +65,7 @@ template <>
 __device__ __forceinline__ void engine_spectra<EngF500>(EngF500& eng, const VsgArgs& A, const RowTask& t,
                                                         const RowTask& tn, bool has_next, float2 (&Cf)[EngF500::NH],
                                                         float2 (&Co)[EngF500::NH]) {
-  if (eng.tab) eng.spectra_tab(t, A.n_pass, A.hop, Cf, Co);
+  if (eng.tab && eng.tab_usable(t.p, A.n_pass)) eng.spectra_tab(t, A.n_pass, A.hop, Cf, Co);
   else eng.spectra(t, tn, has_next, A.w, A.hop, Cf, Co);
 }
 
@@ -556,11 +556,18 @@ __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2*
     nw[2] = tl.ch > pivot ? tl.nwin_f : 0;
     st[3] = t0.a_o;
     nw[3] = t0.ch < pivot ? t0.nwin_o : 0;
+    // an entry holds kTabSub sub-windows: a pass with more (time_window_to_xcorr > 2 wlen) is marked unusable
+    // (every head nwin = -1, nothing transformed) and its row tasks take the plain z = P + i R path
+    const bool fits = nw[0] <= kTabSub && nw[1] <= kTabSub && nw[2] <= kTabSub && nw[3] <= kTabSub;
+    if (!fits) {
+#pragma unroll
+      for (int e = 0; e < kTabEnt; ++e) nw[e] = -1;
+    }
     if (lane < 2 * kTabEnt) head[(int64_t)p * 2 * kTabEnt + lane] = (lane & 1) ? nw[lane >> 1] : st[lane >> 1];
-    // the slices (e, q), q < 3, two per transform; absent ones are zero
+    // the slices (e, q), q < kTabSub, two per transform; absent ones are zero
 #pragma unroll 1
-    for (int s0 = 0; s0 < 3 * kTabEnt; s0 += 2) {
-      const int e0 = s0 / 3, q0 = s0 % 3, e1 = (s0 + 1) / 3, q1 = (s0 + 1) % 3;
+    for (int s0 = 0; s0 < kTabSub * kTabEnt; s0 += 2) {
+      const int e0 = s0 / kTabSub, q0 = s0 % kTabSub, e1 = (s0 + 1) / kTabSub, q1 = (s0 + 1) % kTabSub;
       const bool h0 = q0 < nw[e0], h1 = q1 < nw[e1];
       const float* x0 = tp.piv + st[e0] + q0 * A.hop;
       const float* x1 = tp.piv + st[e1] + q1 * A.hop;
@@ -577,8 +584,8 @@ __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2*
         X = FftPlan<500>::T::run(bufA, bufB, tw, lane);
       }
       const bool l0 = __ballot(nz0 != 0) != 0, l1 = __ballot(nz1 != 0) != 0;
-      float2* o0 = tab + (((int64_t)p * kTabEnt + e0) * 3 + q0) * kTabBins;
-      float2* o1 = tab + (((int64_t)p * kTabEnt + e1) * 3 + q1) * kTabBins;
+      float2* o0 = tab + (((int64_t)p * kTabEnt + e0) * kTabSub + q0) * kTabBins;
+      float2* o1 = tab + (((int64_t)p * kTabEnt + e1) * kTabSub + q1) * kTabBins;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int f = lane + 64 * j;

@@ -253,13 +253,17 @@ struct EngStockham {
 //   e = 2: the forward trajectory window of the last gather row, e = 3: the other-side trajectory window
 //   of the first gather row (the far rows' clamped windows).
 // A row side whose (start, nwin) equals its entry's transforms only its receivers, two per complex FFT.
+// An entry holds kTabSub = 3 sub-windows (the reference's default time_window_to_xcorr = 2 wlen: nwin = 3).
+// A pass with a longer side is marked unusable in the head (every nwin = -1; tab_usable() is false) and
+// its row tasks take the plain path.
 constexpr int kTabEnt = 4;
+constexpr int kTabSub = 3;
 constexpr int kTabBins = 256;  // bins f <= 250 (P / 2: the halving of z's separation folded in, exact);
                                 // [255].x = 1 when the slice has a non-zero sample
-constexpr int64_t kTabPassF2 = (int64_t)kTabEnt * 3 * kTabBins;  // float2 per pass
+constexpr int64_t kTabPassF2 = (int64_t)kTabEnt * kTabSub * kTabBins;  // float2 per pass
 
 __device__ __forceinline__ const float2* tab_slice(const float2* tab, int p, int e, int q) {
-  return tab + (((int64_t)p * kTabEnt + e) * 3 + q) * kTabBins;
+  return tab + (((int64_t)p * kTabEnt + e) * kTabSub + q) * kTabBins;
 }
 // (start, nwin) of every entry: int32 [n_pass][kTabEnt][2] after the spectra
 __device__ __forceinline__ const int32_t* tab_head(const float2* tab, int n_pass) {
@@ -308,6 +312,11 @@ struct EngF500 {
     bufB = bufA + N;
   }
   static __device__ void block_init(char* lds) { init_twiddles<N>(reinterpret_cast<float2*>(lds)); }
+
+  // the pass's table entries hold all its sub-windows (head nwin of entry 0 >= 0)
+  __device__ __forceinline__ bool tab_usable(int p, int n_pass) const {
+    return sld(tab_head(tab, n_pass) + (int64_t)p * kTabEnt * 2 + 1) >= 0;
+  }
 
   static __device__ __forceinline__ int bin(int l, int j) {
     if (j < 3) return l <= 50 ? l + 100 * j : -1;
@@ -581,7 +590,7 @@ struct EngF500 {
     const bool other = (A.flags & kFlagOtherSide) != 0;
     // lane k < n: pass order[b + k] (the passes' table entries in flight together: one load latency)
     const bool act = lane < n;
-    int p = 0, row0 = 0, piv = 0, a = 0, L = 0, Lo = 0, h4 = -1, h5 = -1;
+    int p = 0, row0 = 0, piv = 0, a = 0, L = 0, Lo = 0, h1 = 0, h4 = -1, h5 = -1;
     float sf = 0.f, wp = 0.f;
     if (act) {
       p = order[b + lane];
@@ -592,6 +601,7 @@ struct EngF500 {
       L = seg[1];
       Lo = seg[3];
       const int32_t* head = tab_head(tab, A.n_pass) + (int64_t)p * kTabEnt * 2;
+      h1 = head[1];
       h4 = head[4];
       h5 = head[5];
       sf = scales[2 * p];
@@ -610,7 +620,7 @@ struct EngF500 {
       ff *= sf;
       w = wp * ff;
     }
-    const bool good = !act || (nwo == 0 && nwf == W && shf == shf0 && mf && isfinite(w));
+    const bool good = !act || (h1 >= 0 && nwo == 0 && nwf == W && shf == shf0 && mf && isfinite(w));
     if (__ballot(!good) != 0) return false;
     if (W == 0) return true;  // no sub-windows on any pass: the row adds nothing
     // per-pass sources in lane k: receiver slice and table slice of sub-window 0, factor

@@ -20,14 +20,12 @@ import torch.distributed as dist
 
 
 def shard_passes(slots, world, rank):
-    """Indices of the passes owned by `rank`: each class dealt round-robin, so every rank gets the
-    same share of every class (load balance and identical per-class work)."""
+    """Indices of the passes owned by `rank`: the passes sorted by class are dealt round-robin, so every
+    rank gets the same share of every class (within one pass) and the rank totals differ by at most one
+    pass (a per-class deal that always starts at rank 0 would give rank 0 one extra pass per class)."""
     slots = np.asarray(slots)
-    idx = []
-    for s in np.unique(slots):
-        members = np.flatnonzero(slots == s)
-        idx.append(members[rank::world])
-    return np.sort(np.concatenate(idx)) if idx else np.zeros(0, dtype=np.int64)
+    order = np.argsort(slots, kind="stable")
+    return np.sort(order[rank::world])
 
 
 def global_counts(slots, n_slot):

@@ -222,7 +222,7 @@ class VsgPlan:
             raise ValueError("time slices outside the window: the passes' t_axis does not match the window's "
                              f"{n_t} samples")
         self._dev = {}
-        self._ws = {}  # device -> stack-launch workspace (vsg.spectra_workspace)
+        self._ws = {}  # (device, stream) -> stack-launch workspace (vsg.spectra_workspace)
 
     @classmethod
     def from_trajectories(cls, x_axes, t_axes, veh_xs, veh_ts, prm: VsgParams, n_ch: int, n_t: int):
@@ -312,7 +312,7 @@ class DevicePlan:
             self.seg_tab = torch.empty((n, self.R, 2, 2), dtype=torch.int32, device=dev)
         self.status = torch.empty(n, dtype=torch.int32, device=dev)
         self.geoms = None
-        self._ws = {}  # device -> stack-launch workspace, shared by the slices (their launches are stream-ordered)
+        self._ws = {}  # (device, stream) -> stack-launch workspace, shared by the slices (same-stream launches are ordered)
         if derive:
             self.derive()
 
@@ -514,7 +514,7 @@ class UnitPlan(VsgPlan):
                              f"{n_t} samples")
         self.geoms = None
         self._dev = {}
-        self._ws = {}  # device -> stack-launch workspace (vsg.spectra_workspace)
+        self._ws = {}  # (device, stream) -> stack-launch workspace (vsg.spectra_workspace)
 
     @classmethod
     def concat(cls, plans):

@@ -60,20 +60,32 @@ class _DeviceView:
             d[...] = self.t.to("cpu").numpy()
 
 
+_DESIGNS = {}
+
+
+def _design(dt, flo, fhi, dev):
+    """(sos, zi, padlen) of bandpass_data's filter and their device copies, cached per (dt, band, device):
+    the design is a pure function of its arguments (the reference redesigns it per call)."""
+    key = (float(dt), float(flo), float(fhi), str(dev))
+    if key not in _DESIGNS:
+        sos = butter_bandpass_sos(dt, flo, fhi)
+        zi = scipy.signal.sosfilt_zi(sos)
+        _DESIGNS[key] = (sos, _padlen(sos), torch.from_numpy(np.ascontiguousarray(sos, dtype=np.float64)).to(dev),
+                         torch.from_numpy(np.ascontiguousarray(zi, dtype=np.float64)).to(dev))
+    return _DESIGNS[key]
+
+
 def bandpass_inplace(data, dt, flo, fhi):
-    sos = butter_bandpass_sos(dt, flo, fhi)
-    zi = scipy.signal.sosfilt_zi(sos)
-    padlen = _padlen(sos)
     v = _DeviceView(data)
     t = v.t
     n_t = t.shape[-1]
     rows = t.reshape(-1, n_t)
+    dev = t.device
+    sos, padlen, sos_t, zi_t = _design(dt, flo, fhi, dev)
     if n_t <= padlen:
         raise ValueError(f"The length of the input vector x must be greater than padlen, which is {padlen}.")
-    dev = t.device
-    sos_t = torch.from_numpy(np.ascontiguousarray(sos, dtype=np.float64)).to(dev)
-    zi_t = torch.from_numpy(np.ascontiguousarray(zi, dtype=np.float64)).to(dev)
-    work = torch.empty((rows.shape[0], n_t + 2 * padlen), dtype=torch.float64, device=dev)
+    nbytes = int(_lib.load().dvh_sosfiltfilt_workspace(rows.shape[0], n_t, len(sos), padlen))
+    work = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=dev)
     _lib.call("dvh_sosfiltfilt", _lib.ptr(rows), v.dtype, rows.shape[0], rows.stride(0), n_t, _lib.ptr(sos_t),
               len(sos), padlen, _lib.ptr(zi_t), _lib.ptr(work), _lib.stream_of(dev))
     v.write_back()
@@ -120,7 +132,7 @@ def mute_along_time(window, alpha=0.3):
 
 
 def surface_wave_preprocessing(data, dt, method="surface_wave", flo=1.2, fhi=30, impute_noise_traces=True,
-                               noise_threshold=5, impute_empty_traces=True, return_indices=False):
+                               noise_threshold=5, impute_empty_traces=True, return_indices=False, _phases=None):
     """TimeLapseImaging._preprocessing_for_surface_waves (apis/timeLapseImaging.py:51-71) of a
     continuous record [n_ch, n_t] -> ``data_for_imaging`` (a new array; the input is left as is):
     bandpass_data(flo, fhi) (dvh_sosfiltfilt), then find_noise_idx / impute_noisy_trace for an empty
@@ -140,13 +152,18 @@ def surface_wave_preprocessing(data, dt, method="surface_wave", flo=1.2, fhi=30,
         t = torch.from_numpy(np.array(host, dtype=dt_keep, copy=True)).to(default_device())
     if t.dim() != 2:
         raise ValueError("data must be [n_ch, n_t]")
+    ev = (lambda k: _phases.setdefault(k, torch.cuda.Event(enable_timing=True)).record()) if _phases is not None \
+        else (lambda k: None)  # timing hook (bench.py --workload prep)
+    ev("bandpass0")
     bandpass_inplace(t, dt, flo, fhi)
+    ev("bandpass1")
     dev = t.device
     stats = torch.empty(2 * t.shape[0], dtype=torch.float64, device=dev)
     idx = torch.zeros(2, dtype=torch.int32, device=dev)
     flags = (1 if impute_empty_traces else 0) | (2 if impute_noise_traces else 0) | (4 if method == "surface_wave" else 0)
     _lib.call("dvh_trace_cleanup", _lib.ptr(t), 0 if t.dtype == torch.float32 else 1, t.shape[0], t.stride(0),
               t.shape[1], flags, float(noise_threshold), _lib.ptr(stats), _lib.ptr(idx), _lib.stream_of(dev))
+    ev("cleanup1")
     out = t if on_device else t.cpu().numpy()
     if return_indices:
         return out, tuple(int(i) for i in idx.cpu())

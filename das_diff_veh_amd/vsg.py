@@ -32,9 +32,12 @@ def spectra_workspace(plan: VsgPlan, device, cache: dict | None = None, table: b
     if nbytes <= 0:
         return None
     if cache is not None:
-        ws = cache.get(str(device))
+        # one workspace per (device, stream): a launch on another stream must not overwrite the table a
+        # launch still in flight on this one reads
+        key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+        ws = cache.get(key)
         if ws is None or ws.numel() * 4 < nbytes:
-            ws = cache[str(device)] = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
+            ws = cache[key] = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
         return ws
     return torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=device)
 
@@ -173,6 +176,8 @@ def vsg_stack_validated(windows: torch.Tensor, plan: VsgPlan, schedule: StackSch
     n_ch = windows.shape[1] if scan is None else scan.n_ch
     if n_ch < plan.R:
         raise ValueError("windows narrower than the gather")
+    if scan is not None and scan.n_win and (scan.first_row.min() < 0 or scan.first_row.max() + scan.n_ch > windows.shape[1]):
+        raise ValueError("scan windows reach outside the record rows")
     pass_tab, seg_tab = plan.device_tables(windows.device)
     order, chunk_tab, weights = schedule.device_tables(windows.device)
     if out is None:

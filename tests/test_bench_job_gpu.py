@@ -119,3 +119,50 @@ def test_synth10k_full_job_properties(device):
     assert float((total - fused).abs().max()) <= 1e-5 * scale
     bench.step(job, 1, fused=True)
     assert float((job.stack - fused).abs().max()) <= 1e-5 * scale
+
+
+def test_sliding_job(device):
+    """bench.build_sliding as built (configs[3]'s job at a reduced size): per-batch trajectories over a resident
+    pool, (class, pivot) slots with the fixed 20 / 25 m/s class edges, batches merged into one UnitPlan.concat
+    launch, every window validated through the UnitScan tiling.  Every used slot's stack equals the oracle's
+    mean over that slot's units -- each unit imaged at its own pivot +- 200 m on its pool window with its own
+    batch's trajectory (apis/virtual_shot_gather.py:165-192) -- and its f-v image equals the oracle's."""
+    import bench
+    from oracle import disp as odisp
+    from oracle import vsg as ovsg
+    wl = dict(bench.WORKLOADS["sliding"], n_total=6, pool=3, n_ch=600, merge=2, gen_chunk=3)
+    job = bench.build_sliding(wl, device, 1, 0, "weak", chunk=2)
+    assert len(job.batches) == 1 and job.batches[0].n_merged == 2  # 2 batches of 3 passes, one merged launch
+    bench.step(job, 1)
+    cu = job.cpu_units
+    x_axis, t_axis, pch, half = cu["x_axis"], cu["t_axis"], cu["pch"], cu["half"]
+    wins = job.windows.double().cpu().numpy()
+    n_slot = job.stack.shape[0]
+    per_slot = [[] for _ in range(n_slot)]
+    axes = {}
+    for b in job.batches:
+        u0 = 0
+        for k in range(b.n_merged):
+            plan, trk = job.plans[b.first_batch + k], job.trks[b.first_batch + k]
+            for u in range(plan.n_pass):
+                q, j = int(plan.unit_window[u]), int(plan.unit_pivot[u])
+                p = float(x_axis[pch[j]])
+                o = dict(data=wins[q], x_axis=x_axis, t_axis=t_axis, veh_state_x=trk[q][0], veh_state_t=trk[q][1])
+                g, gx, gt = ovsg.virtual_shot_gather(o, include_other_side=True, norm=False, pivot=p,
+                                                     start_x=p - half, end_x=p + half, wlen=2)
+                per_slot[int(b.slots[u0 + u])].append(g)
+                axes[int(b.slots[u0 + u])] = (gx, gt)
+            u0 += plan.n_pass
+        assert u0 == b.plan.n_pass
+    used = [s for s in range(n_slot) if per_slot[s]]
+    assert len(used) >= 4
+    got = job.stack.double().cpu().numpy()
+    fv = job.fv.cpu().numpy()
+    for s in range(n_slot):
+        if not per_slot[s]:
+            assert not np.any(got[s]), s  # an empty slot stays zero
+            continue
+        ref = ovsg.stack(per_slot[s])
+        assert gio.gather_rel_err(got[s], ref) < TOL, s
+        fref = odisp.compute_disp_image(ref, *axes[s], start_x=-200, end_x=0)
+        assert np.abs(fv[s] - fref).max() / np.abs(fref).max() < TOL, s

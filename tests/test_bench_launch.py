@@ -41,6 +41,21 @@ def test_launcher_parent_never_imports_torch():
     assert rank0["MASTER_ADDR"] == "127.0.0.1" and int(rank0["MASTER_PORT"]) > 0
 
 
+def test_failing_rank_ends_the_launch():
+    """Rank 1 exits 3 while ranks 0 and 2 block (as ranks waiting in a collective for a dead peer do): the
+    launching process stops them and exits non-zero within seconds, naming the rank and its stderr."""
+    import time
+    env = _env()
+    env["DVH_DRY_FAIL"] = "1:3"
+    t0 = time.time()
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--launch-dry-run"], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert time.time() - t0 < 60
+    assert out.returncode == 3, (out.returncode, out.stderr)
+    assert "rank 1 exited with 3" in out.stderr
+    assert "[dry-run] rank 1 fails with 3" in out.stderr  # the failing rank's stderr tail
+
+
 def test_world_size_mismatch_exits_nonzero():
     env = _env()
     env["WORLD_SIZE"] = "2"

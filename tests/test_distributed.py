@@ -79,6 +79,12 @@ def test_shard_balance():
     for s in range(3):
         per = [np.sum(slots[p] == s) for p in parts]
         assert max(per) - min(per) <= 1
+    # rank totals within one pass: 10 240 speed-tercile passes over 2 ranks are 5 120 each (the bench's strong
+    # job then cuts into whole pool-sized batches)
+    sizes = [p.size for p in parts]
+    assert max(sizes) - min(sizes) <= 1
+    terc = np.repeat([0, 1, 2], [3414, 3413, 3413])
+    assert [shard_passes(terc, 2, r).size for r in range(2)] == [5120, 5120]
 
 
 def _fail_worker(rank, world, port, q):

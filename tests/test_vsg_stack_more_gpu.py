@@ -138,3 +138,35 @@ def test_pivot_table_matches_per_subwindow_transforms(device, kw):
         m = np.isfinite(a)
         for s in range(2):
             assert gio.gather_rel_err(np.where(m[s], a[s], 0.0), np.where(m[s], b[s], 0.0)) < 1e-5, (s, kw)
+
+
+@pytest.mark.parametrize("twin", [5, 6])
+@pytest.mark.parametrize("kw", [dict(include_other_side=True, norm=False), dict(include_other_side=True),
+                                dict(include_other_side=False, norm=False)])
+def test_long_xcorr_window_stack(device, twin, kw):
+    """time_window_to_xcorr = 5 / 6 at w = 500 gives nwin = 4 / 5 sub-windows per side, more than the pivot-slice
+    table's entries hold (3): such passes are marked unusable by the table kernel and take the plain
+    per-sub-window path.  Stack with and without the table, and the validated launch, equal the oracle."""
+    from das_diff_veh_amd import vsg
+    from oracle import vsg as ovsg
+    g, wins, prm, plan, data = _fixture_batch(device, time_window_to_xcorr=twin, **kw)
+    assert plan.w == 500 and int(twin / 0.003999999999997783) >= 1250
+    slots = np.arange(plan.n_pass) % 2
+    sched = vsg.StackSchedule(slots, 2, chunk=2)
+    sc = vsg.vsg_scales(data, plan)
+    a = vsg.vsg_stack(data, plan, sched, scales=sc, table=True).double().cpu().numpy()
+    b = vsg.vsg_stack(data, plan, sched, scales=sc, table=False).double().cpu().numpy()
+    host = data.double().cpu().numpy()
+    for s in range(2):
+        refs = []
+        for i in np.flatnonzero(slots == s):
+            o = gio.oracle_window(g, i)
+            o["data"] = host[i]
+            refs.append(ovsg.virtual_shot_gather(o, time_window_to_xcorr=twin, **kw, **KW)[0])
+        ref = ovsg.stack(refs)
+        assert gio.gather_rel_err(a[s], ref) < TOL, (s, twin, kw)
+        assert gio.gather_rel_err(b[s], ref) < TOL, (s, twin, kw)
+    if plan.flags & 6:
+        v = vsg.vsg_stack_validated(data, plan, sched, scales=vsg.vsg_scales(data, plan, validity=False))
+        assert np.allclose(v.double().cpu().numpy(), a, rtol=0, atol=1e-6 * np.abs(a).max())
+
