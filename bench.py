@@ -59,7 +59,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="synth10k",
-                    choices=("synth10k", "weights", "speeds", "sliding", "timelapse", "bootstrap", "prep"))
+                    choices=("synth10k", "weights", "speeds", "sliding", "timelapse", "bootstrap", "prep",
+                             "speeds-host"))
     ap.add_argument("--scaling", default=None, choices=("weak", "strong", "both"),
                     help="weak: every rank its own job; strong: one job split over the ranks; both (default for "
                          "N > 1): the weak line with the strong (fixed-job) measurement beside it")
@@ -71,6 +72,9 @@ def parse_args(argv=None):
     ap.add_argument("--separate-validity", action="store_true",
                     help="window_sumsq launch per batch instead of the validity scan inside the stack launch")
     ap.add_argument("--layout-out", default=None, help="write the launch layout (JSON) for tools/pmc_summary.py")
+    ap.add_argument("--w499", action="store_true",
+                    help="synth10k / weights / speeds on time axes whose dt = 0.004000000000001336 (w = int(wlen / dt) = "
+                         "499, the reference's other operating point: zero-padded 1 024-point transforms)")
     ap.add_argument("--launch-dry-run", action="store_true",
                     help="test hook: the ranks launch_ranks starts print their rank environment instead of benching")
     return ap.parse_args(argv)
@@ -178,7 +182,7 @@ sys.path.insert(0, ROOT)
 from das_diff_veh_amd.disp import DispPlan, fk_grid, fv_from_fk  # noqa: E402
 from das_diff_veh_amd.distributed import allreduce_stacks, max_over_ranks, shard_passes  # noqa: E402
 from das_diff_veh_amd.plan import DevicePlan, VsgParams  # noqa: E402
-from das_diff_veh_amd.synth import TRACK_DT, synth_batch_device  # noqa: E402
+from das_diff_veh_amd.synth import DT_W499, DT_W500, TRACK_DT, synth_batch_device  # noqa: E402
 from das_diff_veh_amd.vsg import StackSchedule, vsg_scales, vsg_stack, vsg_stack_validated, window_sumsq  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -206,6 +210,11 @@ WORKLOADS = {
                            "1-25 Hz, 200-1200 m/s) of 512 gathers of 25 ch x 500 lags per step and rank (a day's "
                            "stacks at 512 pivots): time DFT + channel contraction on the fp64 MFMA pipe, FITPACK "
                            "bilinear + Savitzky-Golay (fp64 MFMA); every rank images its own days"),
+    "speeds-host": dict(kind="host", config="configs[0]-shape, host-fed", classes=(330, 1442, 336), n_ch=60, n_t=5500,
+                        desc="configs[0]-shape through the drop-in API as a notebook calls it: "
+                             "VirtualShotGathersFromWindows(windows_<class>).get_images(include_other_side=True, pivot=700, "
+                             "start_x=500, end_x=900, wlen=2) for fast / mid / slow (330 / 1,442 / 336 NumPy float32 "
+                             "windows of 60 x 5,500 in host memory), each class's avg_image back on the host"),
     "bootstrap": dict(kind="bootstrap", config="SURVEY §8(f) row 1", n=1442, max_size=60, bt_times=30,
                       desc="the notebooks' convergence_test (imaging_diff_speed.ipynb#cell30-31) for one class: 1,442 "
                            "passes of 60 x 5,500 (pivot 700 m, 500-900 m), bt_size 1..60 x 30 resamples, 4 ridge modes "
@@ -271,6 +280,7 @@ def build_pool(wl, device, world, rank, scaling, chunk):
     pool = -(-n_loc_pre // n_bat) if n_loc_pre else wl["pool"]
     t0 = time.time()
     job.windows, x_axis, t_axis, _, _ = synth_batch_device(pool, n_ch=n_ch, n_t=n_t, pivot=pivot, seed=1000 * rank + 3,
+                                                           t0=wl.get("t0", DT_W500),
                                                            device=device, x_first=wl["x_first"], track_half=10,
                                                            chunk=wl["gen_chunk"])
     job.t_gen = time.time() - t0
@@ -358,6 +368,7 @@ def build_resident(wl, device, world, rank, scaling, chunk):
         if k == 0:
             continue
         _, x_axis, t_axis, trk, _ = synth_batch_device(k, n_ch=n_ch, n_t=n_t, pivot=pivot, seed=1000 * rank + 17 * i + 3,
+                                                       t0=wl.get("t0", DT_W500),
                                                        device=device, track_half=wl["track_half"],
                                                        chunk=wl["gen_chunk"], out=job.windows[o:o + k])
         x_axes[o:o + k], piv[o:o + k], sx[o:o + k], ex[o:o + k] = x_axis, pivot, start_x, end_x
@@ -691,10 +702,13 @@ def cpu_baseline_sliding(job, budget_s=20.0, workers=None):
 
 def layout_of(job, args, scaling):
     """What one profiled launch of the stack kernel covers (PMC counters are per launch)."""
-    return {"workload": args.workload, "chunk": args.chunk, "scaling": scaling,
-            "validity": "separate" if args.separate_validity else "fused",
-            "passes_per_launch": [int(b.plan.n_pass) for b in job.batches][:1],
-            "launches_per_step": len(job.batches)}
+    lay = {"workload": args.workload, "chunk": args.chunk, "scaling": scaling,
+           "validity": "separate" if args.separate_validity else "fused",
+           "passes_per_launch": [int(b.plan.n_pass) for b in job.batches][:1],
+           "launches_per_step": len(job.batches)}
+    if job.batches[0].plan.w != 500:
+        lay["w"] = int(job.batches[0].plan.w)
+    return lay
 
 
 def pmc_lookup(kernel, layout, key):
@@ -894,12 +908,19 @@ def prep_main(args, world, rank, device):
     cl = float(np.mean([e["bandpass1"].elapsed_time(e["cleanup1"]) for e in evs])) / 1e3
     flop = 2.0 * 9 * n_sec * n_ext * n_ch  # sequential sosfiltfilt: forward + backward passes
     rec_bytes = 4.0 * n_ch * n_t
-    # parity of the step's output against the oracle on a slice of traces (after timing)
+    # parity (after timing): the step's output against the reference's own path on the whole record
+    # (scipy.signal.sosfiltfilt as bandpass_data calls it, then the imputation and norm), and the bandpass
+    # of two traces against the oracle's pure-Python sosfiltfilt restatement (pinned by tests/golden/prep.npz)
+    from das_diff_veh_amd.preprocess import bandpass_inplace
     from oracle import preprocess as oprep
-    host = rec.double().cpu().numpy()
-    ref = oprep.surface_wave_prep(host.astype(np.float32), dt)
+    host = rec.cpu().numpy()
+    ref = oprep.surface_wave_prep(host, dt, scipy_filter=True)
     got = out.double().cpu().numpy()
     err = float(np.abs(got - ref).max() / np.abs(ref).max())
+    bp_dev = rec[[0, 700]].double().clone()
+    bandpass_inplace(bp_dev, dt, 1.2, 30)
+    bp_ref = oprep.bandpass_data(host[[0, 700]], dt, 1.2, 30)
+    err_bp = float(np.abs(bp_dev.cpu().numpy() - bp_ref).max() / np.abs(bp_ref).max())
     res = {
         "metric": "continuous-record preprocessing: records/s (_preprocessing_for_surface_waves, 1,024 ch x 60 s); "
                   "% FP64 roofline of the bandpass",
@@ -919,24 +940,28 @@ def prep_main(args, world, rank, device):
                      "hbm_bytes_model": "record read + y (f64) written and read + record written",
                      "hbm_frac": (2 * rec_bytes + 16.0 * n_ch * n_ext) / bp / 1e9 / HBM_PEAK_GBS},
         "kernels_ms": {"bandpass": bp * 1e3, "trace_cleanup": cl * 1e3},
-        "parity": {"max_rel_err": err, "tol": 2e-6, "reference": "oracle/preprocess.py surface_wave_prep (float32 "
-                                                                  "record, scipy sosfiltfilt)"},
+        "parity": {"max_rel_err": err, "tol": 2e-6,
+                   "reference": "oracle/preprocess.py surface_wave_prep(scipy_filter=True): scipy.signal.sosfiltfilt as "
+                                "bandpass_data calls it, imputation and norm in float64, on the whole record",
+                   "bandpass_rel_err_vs_restatement": err_bp, "bandpass_tol": 1e-10,
+                   "bandpass_check": "traces 0 and 700 in float64 against oracle/preprocess.py's pure-Python sosfiltfilt"},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the oracle (scipy's sosfiltfilt + the reference's imputation / norm) on one core, on trace slices of the
         # same record for ~cpu_budget / 2 s, scaled to the full record
         torch.set_num_threads(1)
-        sub = host[:128].astype(np.float32)
+        sub = host[:128]
         n, t_c = 0, time.time()
-        while time.time() - t_c < args.cpu_budget / 2:
-            oprep.surface_wave_prep(sub, dt)
+        while time.time() - t_c < args.cpu_budget / 2 or n < 2:
+            oprep.surface_wave_prep(sub, dt, scipy_filter=True)
             n += 1
         secs = (time.time() - t_c) / n
         res["cpu_baseline"] = {"value": sub.shape[0] / n_ch / secs, "unit": "records/s", "cores": 1, "kind": "port",
-                               "sample": f"oracle/preprocess.py surface_wave_prep on 128 of the record's traces, {n} runs "
-                                         f"({secs * 1e3:.0f} ms each), scaled x {n_ch // 128} to the 1,024-trace record; "
-                                         f"cpu={platform.processor() or platform.machine()}"}
+                               "sample": f"the reference's path (scipy.signal.sosfiltfilt as bandpass_data calls it + "
+                                         f"oracle/preprocess.py's imputation and norm) on 128 of the record's traces, "
+                                         f"{n} runs ({secs * 1e3:.0f} ms each), scaled x {n_ch // 128} to the 1,024-trace "
+                                         f"record; cpu={platform.processor() or platform.machine()}"}
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -1078,6 +1103,86 @@ def bootstrap_main(args, world, rank, device):
         dist.destroy_process_group()
 
 
+def host_main(args, world, rank, device):
+    """The drop-in classes fed from host memory (imaging_diff_speed.ipynb's get_images calls): one step = the
+    three classes' get_images on NumPy windows, their H2D staging (device.stage_windows: pinned double
+    buffers, thread-parallel host copies, asynchronous copies on a side stream) included.  Bound: PCIe.
+    value = windows/s; the roofline is the H2D bandwidth of the step's window bytes."""
+    from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+    from das_diff_veh_amd.apis.imaging_classes import VirtualShotGathersFromWindows
+    wl = WORKLOADS["speeds-host"]
+    n_ch, n_t = wl["n_ch"], wl["n_t"]
+    n = sum(wl["classes"])
+    dev_w, x_axis, t_axis, trk, _ = synth_batch_device(n, n_ch=n_ch, n_t=n_t, pivot=700.0, seed=5 + 1000 * rank,
+                                                       device=device)
+    host = dev_w.cpu().numpy()
+    del dev_w
+    wins = []
+    for i in range(n):
+        w = SurfaceWaveWindow.__new__(SurfaceWaveWindow)  # the tracked trajectory given directly (no tracker arrays)
+        w.data, w.x_axis, w.t_axis = np.ascontiguousarray(host[i]), x_axis, t_axis
+        w.veh_state_x, w.veh_state_t = trk[i]
+        wins.append(w)
+    del host
+    cls = np.repeat(np.arange(3), wl["classes"])
+    per_class = [[wins[i] for i in np.flatnonzero(cls == c)] for c in range(3)]
+    kw = dict(include_other_side=True, pivot=700, start_x=500, end_x=900, wlen=2)
+
+    def run():
+        out = []
+        for ws in per_class:
+            im = VirtualShotGathersFromWindows(ws)
+            im.get_images(**kw)
+            out.append(im.avg_image.XCF_out)
+        return out
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res_imgs = run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = max_over_ranks(elapsed, device)
+    step_s = elapsed / args.steps
+    win_bytes = 4.0 * n * n_ch * n_t
+    # the H2D rate of a pinned 64 MB copy on this box (the bound of a host-fed step)
+    pin = torch.empty(64 << 20, dtype=torch.uint8, pin_memory=True)
+    dst = torch.empty(64 << 20, dtype=torch.uint8, device=device)
+    dst.copy_(pin, non_blocking=True)
+    torch.cuda.synchronize()
+    ta = time.perf_counter()
+    for _ in range(10):
+        dst.copy_(pin, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = 10 * (64 << 20) / (time.perf_counter() - ta) / 1e9
+    res = {
+        "metric": "host-fed vehicle-pass windows/sec (drop-in get_images on NumPy windows, H2D included)",
+        "value": world * n / step_s, "unit": "vehicle-pass windows/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic windows in host memory (NumPy float32)",
+        "config": {"workload": "speeds-host", "baseline_config": wl["config"], "description": wl["desc"],
+                   "windows_per_step": world * n, "window_mb": 4.0 * n_ch * n_t / 1e6,
+                   "parallelism": f"dp{world} (replicas)"},
+        "roofline": {"bound": "pcie", "achieved": win_bytes / step_s / 1e9, "peak": h2d, "unit": "GB/s",
+                     "frac": win_bytes / step_s / 1e9 / h2d, "traffic": None,
+                     "peak_source": "pinned 64 MB H2D copies measured in this run (PCIe Gen5 x16 spec 63 GB/s)",
+                     "pcie_bound_windows_per_s": h2d * 1e9 / (4.0 * n_ch * n_t)},
+        "avg_image_finite": bool(all(np.isfinite(x).all() for x in res_imgs)),
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = _ARGS
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1102,11 +1207,15 @@ def main():
             raise SystemExit(f"[bench] world size {dist.get_world_size()} != --gpus {args.gpus}")
 
     kind = WORKLOADS[args.workload]["kind"]
-    if kind in ("timelapse", "bootstrap", "prep"):
-        return {"timelapse": timelapse_main, "bootstrap": bootstrap_main, "prep": prep_main}[kind](args, world, rank,
-                                                                                                   device)
+    if kind in ("timelapse", "bootstrap", "prep", "host"):
+        return {"timelapse": timelapse_main, "bootstrap": bootstrap_main, "prep": prep_main,
+                "host": host_main}[kind](args, world, rank, device)
     if args.sliding_merge is not None:
         WORKLOADS["sliding"]["merge"] = args.sliding_merge
+    if args.w499:
+        if WORKLOADS[args.workload]["kind"] not in ("pool", "resident"):
+            raise SystemExit("--w499 applies to synth10k / weights / speeds")
+        WORKLOADS[args.workload]["t0"] = DT_W499
     scaling = args.scaling or ("weak" if world == 1 else "both")
     res = measure(args, "strong" if scaling == "strong" else "weak", world, rank, device,
                   cpu=rank == 0 and world == 1 and not args.no_cpu_baseline)

@@ -221,13 +221,6 @@ __device__ __forceinline__ void side_scale(int flags, const RowTask& t, float sf
 
 // Time-domain epilogue of a row: lag permutation, per-pass scales, optional row norm, two-sided
 // average -> G[m] for output lag j = lane + 64 m (post_processing_XCF + VirtualShotGather.__init__).
-// Opaque copy of a per-lane value: index arithmetic derived from it stays where it is used instead
-// of being hoisted to the kernel entry (where, for cold paths, it only occupies registers and gets
-// spilled once per wave).
-__device__ __forceinline__ int opaque(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
 
 template <class E>
 __device__ __forceinline__ void row_epilogue(const E& eng, const VsgArgs& A, const float2* Y, const RowTask& t,
@@ -510,13 +503,133 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
     for (int m = 0; m < NH; ++m) Z[m] = make_float2(0.f, 0.f);
     const float2* Y = eng.inverse(Gh, Z);
     const float inv_n = 1.0f / (float)N;
+    const int lane = opaque(lane_);  // per-task addresses formed here, not held across the task loop
 #pragma unroll
     for (int m = 0; m < NJ; ++m) {
-      const int j = lane_ + 64 * m;
+      const int j = lane + 64 * m;
       if (j < A.w) atomicAdd(o + j, eng.c(Y, j, A.w).x * inv_n);
     }
     wave_sync();
   }
+}
+
+// Stack mode, zero-padded transforms (N >= 2w - 1, w without an exact engine, e.g. w = 499 on real time axes):
+// the circular correlation is the fold c[k] = lin[k] + lin[k - w] of the linear one, so it cannot be phase-
+// ramped in the N-point domain; but folding, the lag permutations and the class sum are linear.  The passes of
+// a (chunk, row) task whose row has the same lag conventions as the chunk's first pass (every pass but those
+// whose pivot row lies on the other side of this row) accumulate their weighted side spectra in registers,
+//   Af += w_p alpha_p f_f,p Cf_p,   Ao += w_p beta_p f_o,p Co_p,
+// then ONE inverse transform of Af + i Ao per task yields both sides' summed, folded correlations, which the
+// epilogue permutes with the chunk's conventions and adds to the stack.  Passes with a row norm (the row's
+// norm needs its own folded correlation), NaN data, non-finite factors or other conventions take the exact
+// per-pass time-domain path.
+template <class E>
+__device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
+                                             const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
+                                             int32_t n_chunk, const float* __restrict__ weight,
+                                             float* __restrict__ stack, int64_t t0, int64_t stride) {
+  const int lane_ = threadIdx.x & 63;
+  constexpr int NJ = E::NJ;
+  constexpr int NH = E::NH;
+  constexpr int N = E::NFFT;
+  const bool other = (A.flags & kFlagOtherSide) != 0;
+  const bool norm = (A.flags & kFlagNorm) != 0;
+  const int w = A.w, h = w / 2;
+  const int64_t n_task = (int64_t)n_chunk * A.R;
+  for (int64_t t = t0; t < n_task; t += stride) {
+    const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
+    const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
+    float* o = stack + ((int64_t)slot * A.R + i) * A.w;
+    float2 Af[NH], Ao[NH];
+#pragma unroll
+    for (int m = 0; m < NH; ++m) Af[m] = Ao[m] = make_float2(0.f, 0.f);
+    bool fs0 = false, os0 = false, any = false;
+    if (b < e) {
+      const RowTask t0 = make_task(A, sld(order + b), i);
+      fs0 = t0.ch <= t0.pivot;
+      os0 = t0.ch >= t0.pivot;
+    }
+    for (int q = b; q < e; ++q) {
+      const int p = sld(order + q);
+      const RowTask task = make_task(A, p, i);
+      float2 Cf[NH], Co[NH];
+      eng.spectra(task, task, false, A.w, A.hop, Cf, Co);
+      const float sf = sld(scales + 2 * p), so = sld(scales + 2 * p + 1), wp = sld(weight + p);
+      const int lane = opaque(lane_);
+      float af = 0.f, ao = 0.f;
+#pragma unroll
+      for (int m = 0; m < NH; ++m) {
+        if (E::bin(lane, m) >= 0) {
+          af += fabsf(Cf[m].x) + fabsf(Cf[m].y);
+          ao += fabsf(Co[m].x) + fabsf(Co[m].y);
+        }
+      }
+      const bool bad = __ballot(isnan(af + ao)) != 0;
+      const bool nzo = other && eng.live_o && (__ballot(ao != 0.f) != 0);
+      float ff = task.nwin_f > 0 ? 1.0f / (float)task.nwin_f : 0.f;
+      float fo = task.nwin_o > 0 ? 1.0f / (float)task.nwin_o : 0.f;
+      side_scale(A.flags, task, sf, so, ff, fo);
+      const bool same = (task.ch <= task.pivot) == fs0 && (task.ch >= task.pivot) == os0;
+      if (norm || bad || !same || !isfinite(ff) || (nzo && !isfinite(fo))) {
+        // exact per-pass time-domain path, added straight to the stack
+        const float2* Y = eng.inverse(Cf, Co);
+        float G[NJ];
+        row_epilogue<E>(eng, A, Y, task, sf, so, lane, G);
+#pragma unroll
+        for (int m = 0; m < NJ; ++m) {
+          const int j = lane + 64 * m;
+          if (j < A.w) atomicAdd(o + j, G[m] * wp);
+        }
+        wave_sync();
+        continue;
+      }
+      // other row finite and not identically zero (row_epilogue's test): the two-sided average
+      const bool ok = nzo && fo != 0.f;
+      const float cf = wp * (ok ? 0.5f : 1.f) * ff, co = ok ? wp * 0.5f * fo : 0.f;
+#pragma unroll
+      for (int m = 0; m < NH; ++m) {
+        Af[m].x += cf * Cf[m].x;
+        Af[m].y += cf * Cf[m].y;
+        Ao[m].x += co * Co[m].x;
+        Ao[m].y += co * Co[m].y;
+      }
+      any = true;
+    }
+    if (!any) continue;
+    // N * (sum of folded forward correlations, sum of folded other-side correlations) at lag k: eng.c(Y, k, w)
+    const float2* Y = eng.inverse(Af, Ao);
+    const float inv_n = 1.0f / (float)N;
+#pragma unroll
+    for (int m = 0; m < NJ; ++m) {
+      const int j = lane_ + 64 * m;
+      if (j < w) {
+        const int kf = fs0 ? pmod(w - 1 - j - h, w) : pmod(j + h + 1, w);
+        float g = eng.c(Y, kf, w).x;
+        if (other) {
+          const int ko = os0 ? pmod(h - 1 - j, w) : pmod(j - h, w);
+          g += eng.c(Y, ko, w).y;
+        }
+        atomicAdd(o + j, g * inv_n);
+      }
+    }
+    wave_sync();
+  }
+}
+
+// occupancy of the padded stack kernel: the N >= 1024 engines hold two accumulated side spectra besides the
+// sub-window's (4 x 9 complex per lane at N = 1024) and would spill at 3 waves / SIMD
+template <class E> struct OccP { static constexpr int v = E::NFFT >= 1000 ? 2 : Occ<E>::v; };
+
+template <class E>
+__global__ __launch_bounds__(64 * E::kWaves, OccP<E>::v) void vsg_stackp_kernel(
+    VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
+    const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
+    float* __restrict__ stack, const float2* __restrict__) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  E eng = make_engine<E>(lds);
+  const int wave = threadIdx.x >> 6;
+  stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave,
+                  (int64_t)gridDim.x * E::kWaves);
 }
 
 template <class E>
@@ -724,8 +837,20 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
                          // correlation is the critical path; 1 / 2 / 3 all measured 127.7 k -> 136 k windows/s on synth10k
 #endif
 
-// Persistent validated stack launch: blocks of kFft correlation waves + kScan scan waves, two per CU.
-template <class E, int kFft, int kScan, int kOcc>
+// The row tasks of a stack launch: frequency-domain stacking with the engine's exact (N = w) transforms, or
+// with a zero-padded one (stackp_tasks).
+template <class E, bool EXACT>
+__device__ __forceinline__ void stack_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
+                                            const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
+                                            int32_t n_chunk, const float* __restrict__ weight, float* __restrict__ stack,
+                                            int64_t t0, int64_t stride) {
+  if constexpr (EXACT) stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride);
+  else stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride);
+}
+
+// Persistent validated stack launch: blocks of kFft correlation waves + kScan scan waves (EngF500: two per CU;
+// the 1 024-point engines' LDS and registers allow one).
+template <class E, int kFft, int kScan, int kOcc, bool EXACT = true>
 __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
     const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
@@ -739,8 +864,8 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
 #endif
-    stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
-                    (int64_t)gridDim.x * kFft);
+    stack_tasks<E, EXACT>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
+                          (int64_t)gridDim.x * kFft);
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -849,7 +974,10 @@ struct VsgKernels {
 
 template <class E, bool EXACT>
 VsgKernels vsg_kernels() {
-  const void* st = (EXACT && DVH_FREQ_STACK) ? (const void*)vsg_stackf_kernel<E> : (const void*)vsg_stack_kernel<E>;
+  const void* st;
+  if constexpr (!DVH_FREQ_STACK) st = (const void*)vsg_stack_kernel<E>;
+  else if constexpr (EXACT) st = (const void*)vsg_stackf_kernel<E>;
+  else st = (const void*)vsg_stackp_kernel<E>;
   return VsgKernels{(const void*)vsg_scales_kernel<E>, (const void*)vsg_gather_kernel<E>, st,
                     E::kBlockBytes + E::kWaves * E::kWaveBytes, E::kWaves};
 }
@@ -969,6 +1097,26 @@ static int cu_count() {
 #define DVH_PIVOT_TABLE 1  // stack launches at w = 500 with the per-pass pivot-slice spectra table
 #endif
 
+// The fused (correlation + validity scan) launch of each transform length: kernel, correlation / scan waves per
+// block, blocks per CU, LDS per block.
+struct VStack {
+  const void* fn;
+  int fft, scan, bpc;
+  size_t lds;
+};
+template <class E, int F, int SC, int OCC, bool EXACT>
+static VStack vstack(int bpc) {
+  return VStack{(const void*)vsg_stackv_kernel<E, F, SC, OCC, EXACT>, F, SC, bpc, E::kBlockBytes + F * E::kWaveBytes};
+}
+static bool get_vstack(int n, VStack* v) {
+  switch (n) {
+    case 500: *v = vstack<EngF500, DVH_VSTACK_FFT, DVH_VSTACK_SCAN, 4, true>(DVH_VSTACK_BPC); return true;
+    case 512: *v = vstack<EngStockham<512, true>, 7, 1, 2, false>(1); return true;
+    case 1024: *v = vstack<EngStockham<1024, true>, 7, 1, 2, false>(1); return true;
+    default: return false;
+  }
+}
+
 static int launch_table(VsgArgs& A, float2* tab, hipStream_t s) {
   const int grid = (int)std::min<int64_t>(((int64_t)A.n_pass + 3) / 4, 8 * (int64_t)cu_count());
   void* args[] = {&A, &tab};
@@ -1008,15 +1156,13 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   if (tab)
     if (int rc = launch_table(A, tab, s)) return rc;
   const int64_t tasks = (int64_t)n_chunk * R;
-  if (n == 500 && DVH_FREQ_STACK) {
-    constexpr int F = DVH_VSTACK_FFT, SC = DVH_VSTACK_SCAN;
-    const void* fn = (const void*)vsg_stackv_kernel<EngF500, F, SC, 4>;
-    const size_t lds = EngF500::kBlockBytes + F * EngF500::kWaveBytes;
-    const int64_t need = (tasks + F - 1) / F;
-    const int grid = (int)(need < DVH_VSTACK_BPC * cu_count() ? (need > 0 ? need : 1) : DVH_VSTACK_BPC * cu_count());
+  VStack v{};
+  if (DVH_FREQ_STACK && get_vstack(n, &v)) {
+    const int64_t need = (tasks + v.fft - 1) / v.fft;
+    const int grid = (int)(need < v.bpc * cu_count() ? (need > 0 ? need : 1) : v.bpc * cu_count());
     void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &tab};
-    if (int rc = launch(fn, grid, F + SC, lds, args, s)) return rc;
-  } else {  // other engines: the scan as its own launch, then the plain stack launch
+    if (int rc = launch(v.fn, grid, v.fft + v.scan, v.lds, args, s)) return rc;
+  } else {  // no fused form: the scan as its own launch, then the plain stack launch
     void* sargs[] = {&A, (void*)&S, &vflag, &counter};
     if (int rc = launch((const void*)window_scan_kernel, 4 * cu_count(), 4, 0, sargs, s)) return rc;
     const int64_t grid = (tasks + k.waves - 1) / k.waves;

@@ -100,6 +100,14 @@ __device__ __forceinline__ RowTask make_task(const VsgArgs& A, int p, int i) {
   return t;
 }
 
+// Opaque copy of a per-lane value: index arithmetic derived from it stays where it is used instead
+// of being hoisted to the kernel entry (where, for per-task paths, it only occupies registers across the
+// whole task loop and gets spilled once per wave).
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // |x| != 0 as a bit mask (NaN included); OR-accumulate, test once per sub-window
 __device__ __forceinline__ uint32_t nzbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
 
@@ -115,8 +123,9 @@ __device__ __forceinline__ void accumulate_cross(float2 Az, float2 Bc, float2& C
 // conj(FFT(conj(W))).  W[N - f] = conj(Cf[f]) + i conj(Co[f]).
 template <class E>
 __device__ __forceinline__ void store_conj_hermitian(float2* buf, const float2 (&Cf)[E::NH], const float2 (&Co)[E::NH],
-                                                     int lane) {
+                                                     int lane_) {
   constexpr int N = E::NFFT;
+  const int lane = opaque(lane_);
 #pragma unroll
   for (int j = 0; j < E::NH; ++j) {
     const int f = E::bin(lane, j);
@@ -151,9 +160,12 @@ struct EngStockham {
   }
   static __device__ void block_init(char* lds) { init_twiddles<N>(reinterpret_cast<float2*>(lds)); }
 
-  __device__ void load(const RowTask& t, int a, int w, float2 (&z)[NJ]) const {
+  // sub-window samples staged in registers; a padded transform (w <= N / 2) only has samples n < N / 2, the
+  // upper half of its input is zero (stored once per sub-window, no registers)
+  static constexpr int NZ = PAD ? (N / 2 + 63) / 64 : NJ;
+  __device__ void load(const RowTask& t, int a, int w, float2 (&z)[NZ]) const {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
+    for (int j = 0; j < NZ; ++j) {
       const int n = lane + 64 * j;
       z[j] = (n < w) ? make_float2(t.piv[a + n], t.rcv[a + n]) : make_float2(0.f, 0.f);
     }
@@ -163,7 +175,7 @@ struct EngStockham {
   __device__ void spectra(const RowTask& t, const RowTask&, bool, int w, int hop, float2 (&Cf)[NH],
                           float2 (&Co)[NH]) {
     const int nq = t.nwin_f + t.nwin_o;
-    float2 z[NJ];
+    float2 z[NZ];
 #pragma unroll
     for (int j = 0; j < NH; ++j) {
       Cf[j] = make_float2(0.f, 0.f);
@@ -174,11 +186,18 @@ struct EngStockham {
     for (int q = 0; q < nq; ++q) {
       uint32_t bp = 0, br = 0;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
+      for (int j = 0; j < NZ; ++j) {
         const int n = lane + 64 * j;
         if (n < N) bufA[n] = z[j];
         bp |= nzbits(z[j].x);
         br |= nzbits(z[j].y);
+      }
+      if (PAD) {
+#pragma unroll
+        for (int j = NZ; j < NJ; ++j) {
+          const int n = lane + 64 * j;
+          if (n < N) bufA[n] = make_float2(0.f, 0.f);
+        }
       }
       const bool live = (__ballot(bp != 0) != 0) && (__ballot(br != 0) != 0);
       if (q + 1 < nq) {
@@ -382,18 +401,19 @@ struct EngF500 {
     wave_sync();
     stockham_stage<N, 20, 5>(bufA, bufB, tw, lane);
     wave_sync();
-    if (lane <= 50) {
+    const int ln = opaque(lane);  // the stage's addresses formed per call, not held in registers between calls
+    if (ln <= 50) {
       float2 XA[5], XB[5];
-      const bool pair = lane >= 1 && lane <= 49;
-      last_bfly_from(bufB, lane, XA);
-      if (pair) last_bfly_from(bufB, 100 - lane, XB);
+      const bool pair = ln >= 1 && ln <= 49;
+      last_bfly_from(bufB, ln, XA);
+      if (pair) last_bfly_from(bufB, 100 - ln, XB);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         // partner X[N - f] of f = l + 100 j is X[(100 - l) + 100 (4 - j)]
         const float2 p0 = XA[(5 - j) % 5], p50 = XA[4 - j], pb = XB[4 - j];
         float2 pa;  // value selects (a select of array elements would become a scratch pointer)
-        pa.x = lane == 0 ? p0.x : (lane == 50 ? p50.x : pb.x);
-        pa.y = lane == 0 ? p0.y : (lane == 50 ? p50.y : pb.y);
+        pa.x = ln == 0 ? p0.x : (ln == 50 ? p50.x : pb.x);
+        pa.y = ln == 0 ? p0.y : (ln == 50 ? p50.y : pb.y);
         acc(j, XA[j], pa);
       }
       if (pair) {
@@ -705,10 +725,11 @@ struct EngF500 {
       });
     }
     // Gh = (-1)^lane (conj on the shared window) U conj(tw[f])
-    const float sg = (lane & 1) ? -1.f : 1.f;
+    const int ln = opaque(lane);
+    const float sg = (ln & 1) ? -1.f : 1.f;
 #pragma unroll
     for (int j = 0; j < NH; ++j) {
-      const int f = bin(lane, j);
+      const int f = bin(ln, j);
       if (f >= 0) {
         const float2 t = tw[f];
         const float2 x = cmul(shf0 ? make_float2(U[j].x, -U[j].y) : U[j], make_float2(t.x, -t.y));

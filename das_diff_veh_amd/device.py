@@ -11,13 +11,80 @@ def default_device():
     return torch.device("cuda", torch.cuda.current_device())
 
 
+# Host windows reach the device through a pipeline (stage_windows): chunks of about STAGE_BYTES are copied
+# by a thread pool into one of two pinned buffers (in the windows' own dtype, no host-side conversion), sent
+# by an asynchronous H2D copy on a side stream, and converted to float32 on the device, so that the host copy
+# of chunk k + 1 runs while chunk k crosses PCIe.
+STAGE_BYTES = 64 << 20
+_STAGE = {}
+
+
+def _stager(device, dtype, nbytes):
+    """(side stream, two pinned host buffers, two device buffers, two events) for chunks of <= nbytes."""
+    key = (str(device), str(dtype))
+    st = _STAGE.get(key)
+    if st is None or st["nbytes"] < nbytes:
+        st = dict(nbytes=nbytes, stream=torch.cuda.Stream(device=device),
+                  pinned=[torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)],
+                  dev=[torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(2)],
+                  free=[torch.cuda.Event() for _ in range(2)])
+        _STAGE[key] = st
+    return st
+
+
+def _pool():
+    import concurrent.futures as cf
+    import os
+    if "pool" not in _STAGE:
+        _STAGE["pool"] = cf.ThreadPoolExecutor(max(1, min(8, os.cpu_count() or 1)))
+    return _STAGE["pool"]
+
+
+def stage_windows(hosts, device, out=None):
+    """Same-shape 2-D NumPy arrays -> one float32 device tensor [n, C, T] (or into ``out``), pipelined:
+    pinned double buffering, thread-parallel host copies, asynchronous H2D on a side stream, float64 ->
+    float32 conversion on the device.  The current stream waits for the copies; the call returns when the
+    last host copy is done (the caller's arrays are free to change afterwards)."""
+    n = len(hosts)
+    shape = hosts[0].shape
+    if any(h.shape != shape for h in hosts):
+        raise ValueError("windows of one batch must share their shape")
+    src = np.float32 if all(h.dtype == np.float32 for h in hosts) else np.float64
+    if out is None:
+        out = torch.empty((n,) + tuple(shape), dtype=torch.float32, device=device)
+    per = int(np.prod(shape)) * np.dtype(src).itemsize
+    k = max(1, min(n, STAGE_BYTES // max(per, 1)))
+    st = _stager(device, src, k * per)
+    pool = _pool()
+    tdt = torch.float32 if src == np.float32 else torch.float64
+    for ci, a in enumerate(range(0, n, k)):
+        kk = min(k, n - a)
+        b = ci & 1
+        st["free"][b].synchronize()  # the H2D that last read this pinned buffer is done
+        view = st["pinned"][b].numpy()[:kk * per].view(src).reshape((kk,) + tuple(shape))
+        list(pool.map(lambda j: np.copyto(view[j], hosts[a + j], casting="unsafe"), range(kk)))
+        with torch.cuda.stream(st["stream"]):
+            pin = st["pinned"][b][:kk * per].view(tdt).view((kk,) + tuple(shape))
+            if src == np.float32:
+                out[a:a + kk].copy_(pin, non_blocking=True)
+            else:
+                d = st["dev"][b][:kk * per].view(tdt).view((kk,) + tuple(shape))
+                d.copy_(pin, non_blocking=True)
+                out[a:a + kk].copy_(d)
+            st["free"][b].record(st["stream"])
+    torch.cuda.current_stream(device).wait_stream(st["stream"])
+    return out
+
+
 def to_device_f32(arrays, device=None):
     """Stack same-shape 2-D arrays (numpy or tensors) into one float32 device tensor [n, C, T]."""
     device = device or default_device()
     if all(isinstance(a, torch.Tensor) for a in arrays):
         return torch.stack([a.to(device=device, dtype=torch.float32) for a in arrays]).contiguous()
-    host = np.stack([np.asarray(a.detach().cpu() if isinstance(a, torch.Tensor) else a, dtype=np.float32)
-                     for a in arrays])
+    hosts = [np.asarray(a.detach().cpu() if isinstance(a, torch.Tensor) else a) for a in arrays]
+    if all(h.dtype in (np.float32, np.float64) and h.ndim == 2 for h in hosts) and hosts:
+        return stage_windows(hosts, device)
+    host = np.stack([np.asarray(h, dtype=np.float32) for h in hosts])
     return torch.from_numpy(host).to(device, non_blocking=False)
 
 

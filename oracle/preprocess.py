@@ -55,6 +55,13 @@ def bandpass_data(data, dt, flo, fhi):
     return np.stack([sosfiltfilt_1d(sos, row) for row in np.asarray(data, dtype=np.float64)])
 
 
+def bandpass_data_scipy(data, dt, flo, fhi):
+    """bandpass_data exactly as the reference calls it (modules/utils.py:179-189: scipy.signal.sosfiltfilt on
+    axis 1, SciPy's compiled sosfilt): the CPU baseline of bench.py --workload prep (the pure-Python
+    restatement above is the checker for small inputs)."""
+    return scipy.signal.sosfiltfilt(butter_sos(dt, flo, fhi), data, axis=1)
+
+
 def tukey(n, alpha):
     """scipy.signal.windows.tukey(n, alpha), sym=True."""
     if n <= 0:
@@ -116,9 +123,10 @@ def impute_noisy_trace(data, noise_idx):
 
 
 def surface_wave_prep(data, dt, method="surface_wave", flo=1.2, fhi=30, impute_noise_traces=True, noise_threshold=5,
-                      impute_empty_traces=True):
-    """TimeLapseImaging._preprocessing_for_surface_waves (apis/timeLapseImaging.py:51-71) -> data_for_imaging."""
-    d = bandpass_data(data, dt, flo, fhi)  # returns the filtered copy
+                      impute_empty_traces=True, scipy_filter=False):
+    """TimeLapseImaging._preprocessing_for_surface_waves (apis/timeLapseImaging.py:51-71) -> data_for_imaging.
+    scipy_filter: bandpass through scipy.signal.sosfiltfilt as the reference calls it (large records)."""
+    d = (bandpass_data_scipy if scipy_filter else bandpass_data)(data, dt, flo, fhi)  # the filtered copy
     if impute_empty_traces:
         impute_noisy_trace(d, find_noise_idx(d, noise_threshold=noise_threshold, empty_tr=True))
     if impute_noise_traces:

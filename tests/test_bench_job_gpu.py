@@ -67,9 +67,11 @@ def test_synth10k_job(device):
     import bench
     wl = dict(bench.WORKLOADS["synth10k"], n_total=6, pool=4, gen_chunk=2)
     job = bench.build_pool(wl, device, 1, 0, "weak", chunk=2)
+    # 6 passes over a nominal pool of 4: two equal batches of 3 (no remainder launch)
     assert len(job.batches) == 2 and job.batches[0].plan.R == 1023
+    assert [b.plan.n_pass for b in job.batches] == [3, 3] and job.windows.shape[0] == 3
     bench.step(job, 1)
-    # pass i of the job lives in pool slot i % 4 during its batch
+    # pass i of the job lives in pool slot i % 3 during its batch
     cs = job.cpu_sets[0]
     slots = np.concatenate([b.slots for b in job.batches])
     wins = job.windows.double().cpu().numpy()
@@ -77,7 +79,7 @@ def test_synth10k_job(device):
     per_slot = [[] for _ in range(3)]
     p = cs["prm"]
     for i, (vx, vt) in enumerate(cs["trk"][:6]):
-        o = dict(data=wins[i % 4], x_axis=cs["x_axis"], t_axis=cs["t_axis"], veh_state_x=vx, veh_state_t=vt)
+        o = dict(data=wins[i % 3], x_axis=cs["x_axis"], t_axis=cs["t_axis"], veh_state_x=vx, veh_state_t=vt)
         per_slot[slots[i]].append(ovsg.virtual_shot_gather(o, include_other_side=True, norm=False, pivot=p.pivot,
                                                            start_x=p.start_x, end_x=p.end_x, wlen=p.wlen)[0])
     refs = [ovsg.stack(g) if g else None for g in per_slot]

@@ -123,8 +123,9 @@ def test_stack_modes(device, fixture, kw, special):
         assert gio.gather_rel_err(got[s], ref) < TOL, (s, kw)
 
 
+@pytest.mark.parametrize("fixture", ["vsg_w500", "vsg_w499"])
 @pytest.mark.parametrize("kind", ["zero", "nan", "inf", "nan_outside_rows", "inf_in_slice", "nan_in_slice"])
-def test_validated_stack_invalid_windows(device, kind):
+def test_validated_stack_invalid_windows(device, kind, fixture):
     """vsg_stack_validated: an all-zero window, or a NaN / inf anywhere in it (also in channels no gather
     row reads), makes its class mean NaN (data / ||data||_F, apis/virtual_shot_gather.py:125); the
     other class is unaffected and equals the oracle."""
@@ -135,7 +136,7 @@ def test_validated_stack_invalid_windows(device, kind):
     from das_diff_veh_amd.plan import VsgParams
     from das_diff_veh_amd.vsg import StackSchedule, vsg_stack_validated
     from oracle import vsg as ovsg
-    g = gio.load("vsg_w500")
+    g = gio.load(fixture)
     n = gio.n_pass(g)
     arrs = [gio.pass_arrays(g, i) for i in range(n)]
     d = arrs[1]["data"].copy()
@@ -155,7 +156,7 @@ def test_validated_stack_invalid_windows(device, kind):
                             VsgParams(include_other_side=True, norm=False, **KW))
         i = geo.pivot_idx - geo.start_idx + 3
         t0, L = geo.seg[i, 0]
-        assert L >= 1000
+        assert L == geo.nsamp and L > 400  # a full-length slice (nsamp = 1000 at w = 500, 999 at w = 499)
         d[geo.start_idx + i, t0 + 400] = np.inf if kind == "inf_in_slice" else np.nan
     arrs[1]["data"] = d
     wins = [SurfaceWaveWindow(**a) for a in arrs]
@@ -164,7 +165,39 @@ def test_validated_stack_invalid_windows(device, kind):
     data = torch.as_tensor(np.stack([w.data for w in wins]), dtype=torch.float32, device=device)
     slots = np.array([i % 2 for i in range(n)])
     got = vsg_stack_validated(data, plan, StackSchedule(slots[idx], 2, chunk=2)).double().cpu().numpy()
+    assert plan.w == (500 if fixture == "vsg_w500" else 499)
     assert np.isnan(got[1]).all()
     refs = [ovsg.virtual_shot_gather(gio.oracle_window(g, i), include_other_side=True, norm=False, **KW)[0]
             for i in range(n) if slots[i] == 0]
     assert gio.gather_rel_err(got[0], ovsg.stack(refs)) < TOL
+
+
+@pytest.mark.parametrize("kw", [dict(include_other_side=True, norm=False), dict(include_other_side=True),
+                                dict(include_other_side=False, norm=False)])
+def test_validated_stack_w499(device, kw):
+    """w = 499 (the reference's dt = 0.004000000000001336 operating point): the fused validated launch (padded
+    1 024-point transforms, frequency-domain class sums, the validity scan in the same launch) equals the
+    oracle's class means, with chunks of 1 (every pass its own task) and of 3."""
+    import torch
+
+    from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+    from das_diff_veh_amd.engine import group_windows
+    from das_diff_veh_amd.plan import VsgParams
+    from das_diff_veh_amd.vsg import StackSchedule, vsg_stack_validated
+    from oracle import vsg as ovsg
+    g = gio.load("vsg_w499")
+    n = gio.n_pass(g)
+    wins = [SurfaceWaveWindow(**gio.pass_arrays(g, i)) for i in range(n)]
+    prm = VsgParams(**kw, **KW)
+    if not (prm.flags & 6):
+        pytest.skip("validated stacking needs norm or norm_amp")
+    (idx, plan), = group_windows(wins, prm, device)[0]
+    assert plan.w == 499
+    data = torch.as_tensor(np.stack([w.data for w in wins]), dtype=torch.float32, device=device)
+    slots = np.array([i % 2 for i in range(n)])
+    refs = [[ovsg.virtual_shot_gather(gio.oracle_window(g, i), **kw, **KW)[0] for i in range(n) if slots[i] == s]
+            for s in range(2)]
+    for chunk in (1, 3):
+        got = vsg_stack_validated(data, plan, StackSchedule(slots[idx], 2, chunk=chunk)).double().cpu().numpy()
+        for s in range(2):
+            assert gio.gather_rel_err(got[s], ovsg.stack(refs[s])) < TOL, (s, chunk, kw)

@@ -20,7 +20,9 @@ import sys
 from collections import defaultdict
 
 KERNELS = ("vsg_stackv_kernel", "vsg_stackf_kernel", "window_scan_kernel", "vsg_invalid_fill_kernel", "vsg_stack_kernel", "vsg_scales_kernel", "window_sumsq_kernel", "pass_geometry_kernel", "tdft_gemm_kernel", "tdft_rows_kernel", "fk_contract_kernel",
-           "fv_kernel", "fv_batch_kernel", "fv_tile_kernel", "fv_mfma_kernel", "read4", "read16", "atomic4")
+           "fv_kernel", "fv_batch_kernel", "fv_tile_kernel", "fv_mfma_kernel", "vsg_stackp_kernel", "vsg_gather_kernel",
+           "sos_block_kernel", "sos_scan_kernel", "sos_transition_kernel", "row_stats_kernel", "impute_kernel",
+           "row_normalize_kernel", "select_mean_kernel", "ridge_kernel", "read4", "read16", "atomic4")
 CALIB_BYTES = {"read4": ("FETCH_SIZE", 1 << 30), "read16": ("FETCH_SIZE", 1 << 30), "atomic4": ("WRITE_SIZE", 256 << 20)}
 
 
