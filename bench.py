@@ -1047,8 +1047,9 @@ def bootstrap_main(args, world, rank, device):
         "config": {"workload": "bootstrap", "baseline_config": wl["config"], "description": wl["desc"], "passes": n,
                    "resamples_per_step": B, "nV": plan.nV, "nF": plan.nF, "gather_rows_imaged": plan.nch,
                    "parallelism": f"dp{world} (classes sharded)"},
-        "step_breakdown_ms": {"gathers": t_gather * 1e3, "resample_stacks": t_sel * 1e3, "dispersion": t_disp * 1e3,
-                              "ridges_and_host": t_ridge * 1e3},
+        "step_breakdown_ms": {"gathers_and_host_draws": t_gather * 1e3, "resample_stacks": t_sel * 1e3,
+                              "dispersion": t_disp * 1e3, "ridges": t_ridge * 1e3,
+                              "host_draws": float(np.mean([e["draw_host_s"] for e in evs])) * 1e3},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_SPEC_TF, "unit": "TFLOP/s",
                      "frac": achieved / FP64_MFMA_SPEC_TF, "frac_of_measured_ceiling": achieved / FP64_MFMA_PEAK_TF,
                      "traffic": None, "kernel": "fv_mfma_kernel" if mfma else "fv_kernel", "launch_ms": t_fv * 1e3,

@@ -18,6 +18,7 @@ index 0 never drawn), so seeding ``random`` reproduces the reference's resamples
 from __future__ import annotations
 
 import random
+import time
 
 import numpy as np
 import torch
@@ -48,6 +49,22 @@ def ridges(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25, vel_m
     ``ref_freq_idx`` indexes the band; ``ref_vel`` is a callable of frequency (or an array over
     the band).  Returns float64 [B, n_band] on the host (and the raw picks before the smoothing
     with return_picks=True)."""
+    return ridges_finish(ridges_launch(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx, sigma, vel_max, ref_vel,
+                                       return_picks))
+
+
+def ridges_finish(pending):
+    """Host results of a ridges_launch (synchronises); raises as the reference does for an empty window."""
+    out, status, picks = pending
+    if int(status.max()) != 0:
+        raise ValueError("attempt to get argmax of an empty sequence (no velocity inside a ridge window)")
+    return (out.cpu().numpy(), picks.cpu().numpy()) if picks is not None else out.cpu().numpy()
+
+
+def ridges_launch(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25, vel_max=400, ref_vel=None,
+                  return_picks=False):
+    """The dvh_ridge launch of ridges() without the synchronising read-back: (out, status, picks) device
+    tensors for ridges_finish, so that several modes' walks are queued before one wait."""
     if not isinstance(fv, torch.Tensor) or not fv.is_cuda or fv.dtype != torch.float32 or fv.dim() != 3:
         raise ValueError("fv must be a float32 device tensor [B, Nvel, Nfreq] (no CPU fallback)")
     freqs = np.asarray(freqs, dtype=np.float64)
@@ -82,9 +99,7 @@ def ridges(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25, vel_m
     _lib.call("dvh_ridge", _lib.ptr(fv), fv.stride(0), B, fv.shape[1], fv.shape[2], c0, nb, _lib.ptr(vel_t), ref,
               float(sigma), float(vel_max), _lib.ptr(vref), _lib.ptr(sg), 25, _lib.ptr(out), _lib.ptr(status),
               _lib.ptr(picks), _lib.stream_of(dev))
-    if int(status.max()) != 0:
-        raise ValueError("attempt to get argmax of an empty sequence (no velocity inside a ridge window)")
-    return (out.cpu().numpy(), picks.cpu().numpy()) if return_picks else out.cpu().numpy()
+    return out, status, picks
 
 
 class GatherCache:
@@ -185,7 +200,10 @@ def convergence(cache: GatherCache, max_size, bt_times, sigma, ref_freq_idx, fre
     into one buffer, one tdft / fk / f-v launch each, one ridge launch per mode), so the host synchronises
     once per mode instead of once per (size, mode).  ``phases`` (optional dict) receives torch events
     around the resample / dispersion / ridge parts for timing."""
+    t_draw = time.perf_counter()
     sels = [draw(cache.n, k, bt_times, rand) for k in range(1, max_size + 1)]
+    if phases is not None:
+        phases["draw_host_s"] = time.perf_counter() - t_draw
     s, e, plan = cache.disp_plan(start_x, end_x)
     B = max_size * bt_times
     ev = (lambda name: phases.setdefault(name, torch.cuda.Event(enable_timing=True)).record()) if phases is not None \
@@ -198,13 +216,14 @@ def convergence(cache: GatherCache, max_size, bt_times, sigma, ref_freq_idx, fre
     fv = fv_from_fk(fk_grid(stacks, plan), plan)
     ev("disp1")
     out = np.empty((len(freq_lb), max_size))
-    for m in range(len(freq_lb)):
-        ref = ref_freq_idx[m] - int(np.sum(FREQS < freq_lb[m]))
-        r = ridges(fv, FREQS, VELS, freq_lb[m], freq_up[m], ref_freq_idx=ref, sigma=sigma[m], vel_max=800,
-                   ref_vel=ref_vel[m])
+    pend = [ridges_launch(fv, FREQS, VELS, freq_lb[m], freq_up[m], ref_freq_idx=ref_freq_idx[m] -
+                          int(np.sum(FREQS < freq_lb[m])), sigma=sigma[m], vel_max=800, ref_vel=ref_vel[m])
+            for m in range(len(freq_lb))]  # every mode's walk queued, one wait below
+    ev("ridge1")
+    for m, pd in enumerate(pend):
+        r = ridges_finish(pd)
         for k in range(max_size):
             out[m, k] = np.sum(np.std(r[k * bt_times:(k + 1) * bt_times], axis=0))
-    ev("ridge1")
     return out
 
 

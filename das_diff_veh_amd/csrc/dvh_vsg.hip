@@ -44,7 +44,7 @@ constexpr int kBlock = 512;  // sumsq kernel
 template <class E> struct Occ { static constexpr int v = 3; };
 template <> struct Occ<EngF500> { static constexpr int v = 4; };
 #ifndef DVH_DIRECT
-#define DVH_DIRECT 1  // EngF500 stack kernels: single-sided row tasks transformed across passes (direct_task)
+#define DVH_DIRECT 1  // fused-engine stack kernels: single-sided row tasks transformed across passes (direct_task)
 #endif
 #ifndef DVH_STACKF_OCC
 #define DVH_STACKF_OCC 0
@@ -55,39 +55,46 @@ template <class E> struct OccF {
   static constexpr int v = DVH_STACKF_OCC ? DVH_STACKF_OCC : (E::kWaves == 4 && E::NFFT <= 500 ? 4 : Occ<E>::v);
 };
 
-// One row task's cross spectra: EngF500 with a bound pivot-spectra table uses it (stack kernels).
+// The engines with fused first / last stages (FusedOps: EngF500, EngP1024) take a per-pass pivot-slice
+// spectra table in the stack kernels and pack single-sided tasks across passes.
+template <class E> struct Fused { static constexpr bool v = false; };
+template <> struct Fused<EngF500> { static constexpr bool v = true; };
+template <> struct Fused<EngP1024> { static constexpr bool v = true; };
+
+// Per-kernel engine setup: the sub-window length (the padded engines mask their loads with it) and the
+// pivot-slice table (stack kernels; nullptr elsewhere).
+template <class E>
+__device__ __forceinline__ void bind_engine(E& e, const VsgArgs& A, const float2* tab) {
+  if constexpr (Fused<E>::v) {
+    e.w = A.w;
+    e.tab = tab;
+  }
+}
+
+// One row task's cross spectra: a fused engine with a bound pivot-spectra table uses it (stack kernels).
 template <class E>
 __device__ __forceinline__ void engine_spectra(E& eng, const VsgArgs& A, const RowTask& t, const RowTask& tn,
                                                bool has_next, float2 (&Cf)[E::NH], float2 (&Co)[E::NH]) {
+  if constexpr (Fused<E>::v) {
+    if (eng.tab && eng.tab_usable(t.p, A.n_pass)) {
+      eng.spectra_tab(t, A.n_pass, A.hop, Cf, Co);
+      return;
+    }
+  }
   eng.spectra(t, tn, has_next, A.w, A.hop, Cf, Co);
 }
-template <>
-__device__ __forceinline__ void engine_spectra<EngF500>(EngF500& eng, const VsgArgs& A, const RowTask& t,
-                                                        const RowTask& tn, bool has_next, float2 (&Cf)[EngF500::NH],
-                                                        float2 (&Co)[EngF500::NH]) {
-  if (eng.tab && eng.tab_usable(t.p, A.n_pass)) eng.spectra_tab(t, A.n_pass, A.hop, Cf, Co);
-  else eng.spectra(t, tn, has_next, A.w, A.hop, Cf, Co);
-}
 
-// A row task whose passes have only a table-served forward side, transformed across passes (EngF500).
-template <class E>
-__device__ __forceinline__ bool engine_direct(E&, const VsgArgs&, const float*, const int32_t*, const float*, int, int,
-                                              int, float2 (&)[E::NH]) {
-  return false;
-}
-template <>
-__device__ __forceinline__ bool engine_direct<EngF500>(EngF500& eng, const VsgArgs& A, const float* scales,
-                                                       const int32_t* order, const float* weight, int b, int e, int i,
-                                                       float2 (&Gh)[EngF500::NH]) {
-  return DVH_DIRECT && eng.tab && eng.direct_task(A, scales, order, weight, b, e, i, Gh);
-}
-
-// Engines that read a per-pass table besides the windows (EngF500: the pivot-slice spectra) get it here.
-template <class E>
-__device__ __forceinline__ void bind_engine(E&, const float2*) {}
-template <>
-__device__ __forceinline__ void bind_engine<EngF500>(EngF500& e, const float2* tab) {
-  e.tab = tab;
+// A row task whose passes have only a table-served forward side, transformed across passes.  RAMP: the exact
+// engines' output-spectrum form; otherwise the forward spectrum sum (*shared: its lag convention).
+template <class E, bool RAMP>
+__device__ __forceinline__ bool engine_direct(E& eng, const VsgArgs& A, const float* scales, const int32_t* order,
+                                              const float* weight, int b, int e, int i, float2 (&Gh)[E::NH],
+                                              bool* shared = nullptr) {
+  if constexpr (Fused<E>::v) {
+    return DVH_DIRECT && eng.tab && eng.template direct_task<RAMP>(A, scales, order, weight, b, e, i, Gh, shared);
+  } else {
+    return false;
+  }
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -141,6 +148,7 @@ __global__ __launch_bounds__(64 * E::kWaves, Occ<E>::v) void vsg_scales_kernel(V
                                                              float* __restrict__ scales) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
+  bind_engine(eng, A, nullptr);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const bool other = (A.flags & kFlagOtherSide) != 0;
@@ -297,6 +305,7 @@ __global__ __launch_bounds__(64 * E::kWaves, Occ<E>::v) void vsg_gather_kernel(V
                                                              float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
+  bind_engine(eng, A, nullptr);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   constexpr int NJ = E::NJ;
@@ -329,6 +338,7 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stack_kernel(V
                                                             float* __restrict__ stack, const float2* __restrict__) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
+  bind_engine(eng, A, nullptr);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   constexpr int NJ = E::NJ;
@@ -407,7 +417,7 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
 #pragma unroll
     for (int m = 0; m < NH; ++m) Gh[m] = make_float2(0.f, 0.f);
     RowTask task = (E::kNextTask && b < e) ? make_task(A, sld(order + b), i) : RowTask{};
-    const bool direct = !norm && engine_direct(eng, A, scales, order, weight, b, e, i, Gh);
+    const bool direct = !norm && engine_direct<E, true>(eng, A, scales, order, weight, b, e, i, Gh);
     for (int q = direct ? e : b; q < e; ++q) {
       const int p = sld(order + q);
       RowTask tn = task;
@@ -543,17 +553,24 @@ __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const flo
     float2 Af[NH], Ao[NH];
 #pragma unroll
     for (int m = 0; m < NH; ++m) Af[m] = Ao[m] = make_float2(0.f, 0.f);
-    bool fs0 = false, os0 = false, any = false;
+    bool fs0 = false, os0 = false, any = false, anyo = false;
     if (b < e) {
       const RowTask t0 = make_task(A, sld(order + b), i);
       fs0 = t0.ch <= t0.pivot;
       os0 = t0.ch >= t0.pivot;
     }
-    for (int q = b; q < e; ++q) {
+    // single-sided tasks with table-served forward slices: receivers packed across passes (fused engines)
+    bool dshared = fs0;
+    const bool direct = !norm && engine_direct<E, false>(eng, A, scales, order, weight, b, e, i, Af, &dshared);
+    if (direct) {
+      fs0 = dshared;
+      any = true;
+    }
+    for (int q = direct ? e : b; q < e; ++q) {
       const int p = sld(order + q);
       const RowTask task = make_task(A, p, i);
       float2 Cf[NH], Co[NH];
-      eng.spectra(task, task, false, A.w, A.hop, Cf, Co);
+      engine_spectra(eng, A, task, task, false, Cf, Co);
       const float sf = sld(scales + 2 * p), so = sld(scales + 2 * p + 1), wp = sld(weight + p);
       const int lane = opaque(lane_);
       float af = 0.f, ao = 0.f;
@@ -594,6 +611,7 @@ __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const flo
         Ao[m].y += co * Co[m].y;
       }
       any = true;
+      anyo |= ok;
     }
     if (!any) continue;
     // N * (sum of folded forward correlations, sum of folded other-side correlations) at lag k: eng.c(Y, k, w)
@@ -605,7 +623,7 @@ __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const flo
       if (j < w) {
         const int kf = fs0 ? pmod(w - 1 - j - h, w) : pmod(j + h + 1, w);
         float g = eng.c(Y, kf, w).x;
-        if (other) {
+        if (other && anyo) {  // (an all-zero Ao's inverse is rounding noise, not the exact 0 the reference adds)
           const int ko = os0 ? pmod(h - 1 - j, w) : pmod(j - h, w);
           g += eng.c(Y, ko, w).y;
         }
@@ -624,9 +642,10 @@ template <class E>
 __global__ __launch_bounds__(64 * E::kWaves, OccP<E>::v) void vsg_stackp_kernel(
     VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
     const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
-    float* __restrict__ stack, const float2* __restrict__) {
+    float* __restrict__ stack, const float2* __restrict__ ptab) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
+  bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6;
   stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave,
                   (int64_t)gridDim.x * E::kWaves);
@@ -639,24 +658,27 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
     float* __restrict__ stack, const float2* __restrict__ ptab) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
-  bind_engine(eng, ptab);
+  bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6;
   stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave,
                   (int64_t)gridDim.x * E::kWaves);
 }
 
-// The pivot-slice spectra table of every pass (EngF500::spectra_tab): one wave per pass forms the
+// The pivot-slice spectra table of every pass (FusedOps::spectra_tab) for engine E: one wave per pass forms the
 // entries' (start, nwin) from the pivot row and the first / last gather rows and transforms their slices
-// pairwise with the Stockham FFT, writing P[f], f <= 250, and each slice's non-zero flag at bin 255.
+// pairwise with the engine's transform (zero-padded past w for the padded engines), writing P[f] / 2, f <= N / 2,
+// and each slice's non-zero flag at bin kTabBins - 1.
+template <class E>
 __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2* __restrict__ tab) {
+  constexpr int N = E::N, BINS = E::kTabBins;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float2* tw = reinterpret_cast<float2*>(lds);
-  init_twiddles<500>(tw);
+  init_twiddles<N>(tw);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float2* bufA = reinterpret_cast<float2*>(lds + sizeof(float2) * 500 + (size_t)wave * sizeof(float2) * 1000);
-  float2* bufB = bufA + 500;
-  int32_t* head = reinterpret_cast<int32_t*>(tab + (int64_t)A.n_pass * kTabPassF2);
+  float2* bufA = reinterpret_cast<float2*>(lds + sizeof(float2) * N + (size_t)wave * sizeof(float2) * 2 * N);
+  float2* bufB = bufA + N;
+  int32_t* head = reinterpret_cast<int32_t*>(tab + (int64_t)A.n_pass * tab_pass_f2<BINS>());
   for (int p = blockIdx.x * 4 + wave; p < A.n_pass; p += gridDim.x * 4) {
     const int row0 = sld(A.pass_tab + 2 * p), pivot = sld(A.pass_tab + 2 * p + 1);
     const RowTask tp = make_task(A, p, pivot - row0), tl = make_task(A, p, A.R - 1), t0 = make_task(A, p, 0);
@@ -687,29 +709,28 @@ __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2*
       uint32_t nz0 = 0, nz1 = 0;
       const float2* X = nullptr;
       if (h0 || h1) {
-        for (int n = lane; n < 500; n += 64) {
-          const float v0 = h0 ? x0[n] : 0.f, v1 = h1 ? x1[n] : 0.f;
+        for (int n = lane; n < N; n += 64) {
+          const bool in = n < A.w;  // the padded engines' zeros past the sub-window
+          const float v0 = (h0 && in) ? x0[n] : 0.f, v1 = (h1 && in) ? x1[n] : 0.f;
           nz0 |= nzbits(v0);
           nz1 |= nzbits(v1);
           bufA[n] = make_float2(v0, v1);
         }
         wave_sync();
-        X = FftPlan<500>::T::run(bufA, bufB, tw, lane);
+        X = FftPlan<N>::T::run(bufA, bufB, tw, lane);
       }
       const bool l0 = __ballot(nz0 != 0) != 0, l1 = __ballot(nz1 != 0) != 0;
-      float2* o0 = tab + (((int64_t)p * kTabEnt + e0) * kTabSub + q0) * kTabBins;
-      float2* o1 = tab + (((int64_t)p * kTabEnt + e1) * kTabSub + q1) * kTabBins;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int f = lane + 64 * j;
+      float2* o0 = tab + (((int64_t)p * kTabEnt + e0) * kTabSub + q0) * BINS;
+      float2* o1 = tab + (((int64_t)p * kTabEnt + e1) * kTabSub + q1) * BINS;
+      for (int f = lane; f < BINS; f += 64) {
         float2 p0 = make_float2(0.f, 0.f), p1 = p0;
-        if (X && f <= 250) {
-          const float2 za = X[f], zc = X[f == 0 ? 0 : 500 - f];
+        if (X && f <= N / 2) {
+          const float2 za = X[f], zc = X[f == 0 ? 0 : N - f];
           // P / 2 of each slice (the consumers separate 2 R from their own transforms)
           p0 = make_float2(0.25f * (za.x + zc.x), 0.25f * (za.y - zc.y));
           p1 = make_float2(0.25f * (za.y + zc.y), -0.25f * (za.x - zc.x));
         }
-        if (f == kTabBins - 1) {
+        if (f == BINS - 1) {
           p0 = make_float2(l0 ? 1.f : 0.f, 0.f);
           p1 = make_float2(l1 ? 1.f : 0.f, 0.f);
         }
@@ -858,7 +879,7 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     const float2* __restrict__ ptab) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
-  bind_engine(eng, ptab);
+  bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (wave < kFft) {
 #if DVH_CORR_PRIO
@@ -1003,7 +1024,7 @@ static bool get_kernels(int w, VsgKernels* k, int* n_out) {
     case 500: *k = vsg_kernels<EngF500, true>(); return true;  // fused-stage Stockham
     case 1000: *k = vsg_kernels<EngStockham<1000, false>, true>(); return true;
     case 512: *k = vsg_kernels<EngStockham<512, true>, false>(); return true;
-    case 1024: *k = vsg_kernels<EngStockham<1024, true>, false>(); return true;
+    case 1024: *k = vsg_kernels<EngP1024, false>(); return true;  // fused-stage padded Stockham
     case 2048: *k = vsg_kernels<EngStockham<2048, true>, false>(); return true;
     default: return false;
   }
@@ -1112,21 +1133,32 @@ static bool get_vstack(int n, VStack* v) {
   switch (n) {
     case 500: *v = vstack<EngF500, DVH_VSTACK_FFT, DVH_VSTACK_SCAN, 4, true>(DVH_VSTACK_BPC); return true;
     case 512: *v = vstack<EngStockham<512, true>, 7, 1, 2, false>(1); return true;
-    case 1024: *v = vstack<EngStockham<1024, true>, 7, 1, 2, false>(1); return true;
+    case 1024: *v = vstack<EngP1024, 7, 1, 2, false>(1); return true;
     default: return false;
   }
 }
 
-static int launch_table(VsgArgs& A, float2* tab, hipStream_t s) {
+// Transform lengths whose engine takes the pivot-slice table: 500 (EngF500) and the padded 1 024 (EngP1024).
+static bool table_engine(int n) { return DVH_PIVOT_TABLE && DVH_FREQ_STACK && (n == 500 || n == 1024); }
+
+template <class E>
+static int64_t table_bytes(int64_t n_pass) {
+  return n_pass * (tab_pass_f2<E::kTabBins>() * (int64_t)sizeof(float2) + 2 * kTabEnt * (int64_t)sizeof(int32_t));
+}
+
+static int launch_table(VsgArgs& A, int n, float2* tab, hipStream_t s) {
   const int grid = (int)std::min<int64_t>(((int64_t)A.n_pass + 3) / 4, 8 * (int64_t)cu_count());
   void* args[] = {&A, &tab};
-  return launch((const void*)vsg_pivot_table_kernel, grid, 4, sizeof(float2) * (500 + 4 * 1000), args, s);
+  if (n == 500)
+    return launch((const void*)vsg_pivot_table_kernel<EngF500>, grid, 4, sizeof(float2) * (500 + 4 * 1000), args, s);
+  return launch((const void*)vsg_pivot_table_kernel<EngP1024>, grid, 4, sizeof(float2) * (1024 + 4 * 2048), args, s);
 }
 
 DVH_API int64_t dvh_vsg_stack_workspace(int32_t n_pass, int32_t w) {
   bool pad;
-  if (choose_fft(w, &pad) != 500 || n_pass <= 0) return 0;
-  return (int64_t)n_pass * (kTabPassF2 * (int64_t)sizeof(float2) + 2 * kTabEnt * (int64_t)sizeof(int32_t));
+  const int n = choose_fft(w, &pad);
+  if (n_pass <= 0 || !table_engine(n)) return 0;
+  return n == 500 ? table_bytes<EngF500>(n_pass) : table_bytes<EngP1024>(n_pass);
 }
 
 DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass,
@@ -1150,11 +1182,11 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   hipStream_t s = (hipStream_t)stream;
   uint32_t* vflag = work;
   uint32_t* counter = work + S.n_win;
-  float2* tab = (n == 500 && DVH_PIVOT_TABLE) ? reinterpret_cast<float2*>(spec_ws) : nullptr;
+  float2* tab = (table_engine(n) && spec_ws) ? reinterpret_cast<float2*>(spec_ws) : nullptr;
   hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t) * ((size_t)S.n_win + 1), s);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
   if (tab)
-    if (int rc = launch_table(A, tab, s)) return rc;
+    if (int rc = launch_table(A, n, tab, s)) return rc;
   const int64_t tasks = (int64_t)n_chunk * R;
   VStack v{};
   if (DVH_FREQ_STACK && get_vstack(n, &v)) {
@@ -1189,9 +1221,9 @@ DVH_API int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stri
   if (!get_kernels(w, &k, &n)) return set_error(-4, "unsupported correlation window length");
   const int64_t tasks = (int64_t)n_chunk * R;
   hipStream_t s = (hipStream_t)stream;
-  float2* tab = (n == 500 && DVH_PIVOT_TABLE && DVH_FREQ_STACK) ? reinterpret_cast<float2*>(spec_ws) : nullptr;
+  float2* tab = (table_engine(n) && spec_ws) ? reinterpret_cast<float2*>(spec_ws) : nullptr;
   if (tab)
-    if (int rc = launch_table(A, tab, s)) return rc;
+    if (int rc = launch_table(A, n, tab, s)) return rc;
   const int64_t grid = (tasks + k.waves - 1) / k.waves;
   void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, &tab};
   return launch(k.stack, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, s);
