@@ -201,7 +201,7 @@ def convergence(cache: GatherCache, max_size, bt_times, sigma, ref_freq_idx, fre
     once per mode instead of once per (size, mode).  ``phases`` (optional dict) receives torch events
     around the resample / dispersion / ridge parts for timing."""
     t_draw = time.perf_counter()
-    sels = [draw(cache.n, k, bt_times, rand) for k in range(1, max_size + 1)]
+    sels = draw_sizes(cache.n, range(1, max_size + 1), bt_times, rand)
     if phases is not None:
         phases["draw_host_s"] = time.perf_counter() - t_draw
     s, e, plan = cache.disp_plan(start_x, end_x)
@@ -228,8 +228,27 @@ def convergence(cache: GatherCache, max_size, bt_times, sigma, ref_freq_idx, fre
 
 
 def draw(n, bt_size, bt_times, rand=random):
-    """The reference's draws: bt_times x random.sample(range(1, n), bt_size)."""
-    return np.array([rand.sample(range(1, n), bt_size) for _ in range(bt_times)], dtype=np.int32)
+    """The reference's draws: bt_times x random.sample(range(1, n), bt_size), bit for bit, formed by the
+    library's host routine from the generator's Mersenne Twister state (dvh_random_sample), which is handed
+    back so that ``rand`` continues exactly as after Python's own calls.  ``rand``: the ``random`` module or a
+    random.Random instance."""
+    return draw_sizes(n, [bt_size], bt_times, rand)[0]
+
+
+def draw_sizes(n, sizes, bt_times, rand=random):
+    """[draw(n, k, bt_times, rand) for k in sizes] with one read and one write-back of the generator state."""
+    for k in sizes:
+        if not 0 <= k <= max(n - 1, 0):
+            raise ValueError("Sample larger than population or is negative")
+    version, mt, gauss = rand.getstate()
+    st = np.array(mt, dtype=np.uint32)
+    outs = []
+    for k in sizes:
+        out = np.empty((bt_times, k), dtype=np.int64)
+        _lib.call("dvh_random_sample", st.ctypes.data, 1, max(n - 1, 0), k, bt_times, out.ctypes.data)
+        outs.append(out.astype(np.int32))
+    rand.setstate((version, tuple(int(v) for v in st), gauss))
+    return outs
 
 
 def save_ridge_npz(file_name, freqs, freq_lb, freq_ub, reference_layout=False, **ridges):

@@ -129,57 +129,139 @@ __global__ __launch_bounds__(64) void sos_transition_kernel(const double* __rest
 }
 
 // Phases A (OUT = false: end states of blocks k < nb - 1 into S) and C (OUT = true: filter from the true start
-// state S[k - 1] and write the outputs: y[i] forward, the trimmed row backward).  Lane g = r * nb + k.
+// state S[k - 1] and write the outputs: y[i] forward, the trimmed row backward).  One wave per 64 consecutive
+// lanes g = r * nb + k.  A lane's block is a run of L samples at its own address, so direct per-lane loads
+// would touch 64 cache lines per instruction; instead the wave moves its 64 runs in chunks of kSosCh samples
+// through an LDS tile: cooperative loads (16 lanes per run: each instruction reads 4 contiguous runs of 16
+// samples), the recursion on the lane's own tile row, and (phase C) the outputs written back into the same
+// tile slots and stored cooperatively, again 16 contiguous samples per 16 lanes.
+constexpr int kSosCh = 16;           // samples per chunk (L is a multiple of 32)
+constexpr int kSosLd = kSosCh + 1;   // tile row stride in doubles: conflict-free own-row reads
 template <typename T, int NS, bool BWD, bool OUT>
-__global__ __launch_bounds__(256) void sos_block_kernel(T* __restrict__ x, double* __restrict__ y, SosGeom G,
-                                                         const double* __restrict__ sos, const double* __restrict__ zi,
-                                                         double* __restrict__ S) {
+__global__ __launch_bounds__(64) void sos_block_kernel(T* __restrict__ x, double* __restrict__ y, SosGeom G,
+                                                        const double* __restrict__ sos, const double* __restrict__ zi,
+                                                        double* __restrict__ S) {
   constexpr int NST = 2 * NS;
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G.n_rows * G.nb) return;
-  const int64_t r = g / G.nb;
-  const int k = (int)(g - r * G.nb);
-  if (!OUT && k == G.nb - 1) return;  // the last block's end state is not needed
-  const SosInput<T, BWD> u = sos_input<T, BWD>(x, y, G, r);
+  __shared__ double tile[64 * kSosLd];
+  const int lane = threadIdx.x;
+  const int64_t n_lanes = G.n_rows * G.nb;
+  const int64_t g0 = (int64_t)blockIdx.x * 64;
+  const int64_t g = g0 + lane;
+  const bool act = g < n_lanes && (OUT || (g % G.nb) != G.nb - 1);  // phase A: no end state of the last block
+  const int64_t r = act ? g / G.nb : 0;
+  const int k = act ? (int)(g - r * G.nb) : 0;
+  const int64_t i0 = (int64_t)k * G.L, i1 = act ? min(i0 + G.L, G.n_ext) : i0;
+  // this lane's part of the cooperative moves: runs s = 4 m + (lane >> 4), samples e = lane & 15 of a chunk
+  const int e = lane & 15;
   SosCoef<NS> c;
   c.load(sos);
   double z0[NS], z1[NS];
   double* Sr = S + g * NST;  // S[r][k]
-  if (k == 0) {
+  if (act && k == 0) {
+    const SosInput<T, BWD> u = sos_input<T, BWD>(x, y, G, r);
     const double u0 = u(0);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      z0[s] = zi[2 * s] * u0;
-      z1[s] = zi[2 * s + 1] * u0;
+    for (int q = 0; q < NS; ++q) {
+      z0[q] = zi[2 * q] * u0;
+      z1[q] = zi[2 * q + 1] * u0;
     }
-  } else if (OUT) {
+  } else if (act && OUT) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      z0[s] = Sr[-NST + 2 * s];
-      z1[s] = Sr[-NST + 2 * s + 1];
+    for (int q = 0; q < NS; ++q) {
+      z0[q] = Sr[-NST + 2 * q];
+      z1[q] = Sr[-NST + 2 * q + 1];
     }
   } else {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) z0[s] = z1[s] = 0.0;
+    for (int q = 0; q < NS; ++q) z0[q] = z1[q] = 0.0;
   }
-  const int64_t i0 = (int64_t)k * G.L, i1 = min(i0 + G.L, G.n_ext);
-  if (!OUT) {
-    for (int64_t i = i0; i < i1; ++i) c.step(z0, z1, u(i));
+  // the longest run of the wave (every block but a row's last has L samples)
+  int64_t n_chunks = 0;
+  {
+    const int64_t len = i1 - i0;
+    int64_t mx = len;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      Sr[2 * s] = z0[s];
-      Sr[2 * s + 1] = z1[s];
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (int64_t)__shfl_xor((long long)mx, o));
+    n_chunks = (mx + kSosCh - 1) / kSosCh;
+  }
+  // run s = 4 m + (lane >> 4) of the wave is lane g0 + s: its (row, block) by stepping 4 lanes per m
+  const int l4 = lane >> 4;
+  const int64_t gl = g0 + l4;
+  const int64_t r_l = gl / G.nb;
+  const int k_l = (int)(gl - r_l * G.nb);
+  // sample i of run (rs, ks): the sequence the pass filters (forward: the odd extension of x; backward: the
+  // forward output reversed)
+  auto in_at = [&](int64_t rs, int64_t i) -> double {
+    if (BWD) return y[rs * G.n_ext + (G.n_ext - 1 - i)];
+    const T* row = x + rs * G.row_stride;
+    const int64_t j = i - G.padlen;
+    if (j >= 0 && j < G.n_t) return (double)row[j];
+    if (j < 0) return 2.0 * (double)row[0] - (double)row[-j];                    // i < padlen
+    return 2.0 * (double)row[G.n_t - 1] - (double)row[2 * (G.n_t - 1) - j];     // past the end
+  };
+  for (int64_t ch = 0; ch < n_chunks; ++ch) {
+    const int64_t cbase = ch * kSosCh;
+    // cooperative load: run s's samples [i0_s + cbase, + kSosCh)
+    {
+      int64_t rs = r_l;
+      int ks = k_l;
+#pragma unroll 4
+      for (int m = 0; m < 16; ++m) {
+        const int sidx = 4 * m + l4;
+        double v = 0.0;
+        if (g0 + sidx < n_lanes) {
+          const int64_t i = (int64_t)ks * G.L + cbase + e;
+          if (i < min((int64_t)(ks + 1) * G.L, G.n_ext)) v = in_at(rs, i);
+        }
+        tile[sidx * kSosLd + e] = v;
+        ks += 4;
+        while (ks >= G.nb) {
+          ks -= G.nb;
+          ++rs;
+        }
+      }
     }
-  } else if (!BWD) {
-    double* yr = y + r * G.n_ext;
-    for (int64_t i = i0; i < i1; ++i) yr[i] = c.step(z0, z1, u(i));
-  } else {
-    T* row = x + r * G.row_stride;
-    // reversed index i is sample n_ext - 1 - i of the extension; the row keeps [padlen, padlen + n_t)
-    for (int64_t i = i0; i < i1; ++i) {
-      const double v = c.step(z0, z1, u(i));
-      const int64_t j = G.n_ext - 1 - i - G.padlen;
-      if (j >= 0 && j < G.n_t) row[j] = (T)v;
+    __syncthreads();
+    const int64_t nn = min((int64_t)kSosCh, i1 - i0 - cbase);
+    if (OUT) {
+      for (int t = 0; t < nn; ++t) tile[lane * kSosLd + t] = c.step(z0, z1, tile[lane * kSosLd + t]);
+    } else {
+      for (int t = 0; t < nn; ++t) c.step(z0, z1, tile[lane * kSosLd + t]);
+    }
+    __syncthreads();
+    if (OUT) {  // cooperative store of the outputs
+      int64_t rs = r_l;
+      int ks = k_l;
+#pragma unroll 4
+      for (int m = 0; m < 16; ++m) {
+        const int sidx = 4 * m + l4;
+        if (g0 + sidx < n_lanes) {
+          const int64_t i = (int64_t)ks * G.L + cbase + e;
+          if (i < min((int64_t)(ks + 1) * G.L, G.n_ext)) {
+            const double v = tile[sidx * kSosLd + e];
+            if (!BWD) {
+              y[rs * G.n_ext + i] = v;
+            } else {
+              // reversed index i is sample n_ext - 1 - i of the extension; the row keeps [padlen, padlen + n_t)
+              const int64_t j = G.n_ext - 1 - i - G.padlen;
+              if (j >= 0 && j < G.n_t) x[rs * G.row_stride + j] = (T)v;
+            }
+          }
+        }
+        ks += 4;
+        while (ks >= G.nb) {
+          ks -= G.nb;
+          ++rs;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (!OUT && act) {
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      Sr[2 * q] = z0[q];
+      Sr[2 * q + 1] = z1[q];
     }
   }
 }
@@ -198,12 +280,34 @@ __global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* _
   double* Sr = S + (act ? r : 0) * (int64_t)G.nb * NST;
   double s = act ? Sr[j] : 0.0;
   const int base = half * 32;
-  for (int k = 1; k < G.nb - 1; ++k) {
-    double acc = act ? Sr[(int64_t)k * NST + j] : 0.0;
+  // the zero-state end states e_k come from memory 8 steps at a time, the next 8 loaded under this group's
+  // arithmetic (a load per step would put one memory latency on the critical path of every step)
+  constexpr int PF = 8;
+  const int kend = G.nb - 1;  // steps k = 1 .. nb - 2
+  double cur[PF], nxt[PF];
 #pragma unroll
-    for (int i = 0; i < NST; ++i) acc += m[i] * __shfl(s, base + i);
-    if (act) Sr[(int64_t)k * NST + j] = acc;
-    s = acc;
+  for (int t = 0; t < PF; ++t) cur[t] = (act && 1 + t < kend) ? Sr[(int64_t)(1 + t) * NST + j] : 0.0;
+  for (int kb = 1; kb < kend; kb += PF) {
+#pragma unroll
+    for (int t = 0; t < PF; ++t) {
+      const int k = kb + PF + t;
+      nxt[t] = (act && k < kend) ? Sr[(int64_t)k * NST + j] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < PF; ++t) {
+      const int k = kb + t;
+      if (k < kend) {
+        // M s in four partial sums (a 5-deep instead of a 20-deep chain of dependent FMAs per step)
+        double pa[4] = {cur[t], 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < NST; ++i) pa[i & 3] += m[i] * __shfl(s, base + i);
+        const double acc = (pa[0] + pa[1]) + (pa[2] + pa[3]);
+        if (act) Sr[(int64_t)k * NST + j] = acc;
+        s = acc;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < PF; ++t) cur[t] = nxt[t];
   }
 }
 
@@ -241,16 +345,16 @@ static int sosfiltfilt_blocks(T* x, const SosGeom& G, const double* sos, const d
   double* S = y + G.n_rows * G.n_ext;
   double* M = S + G.n_rows * G.nb * NST;
   const int64_t lanes = G.n_rows * G.nb;
-  const dim3 grid((unsigned)((lanes + 255) / 256)), scan_grid((unsigned)((G.n_rows + 1) / 2));
+  const dim3 grid((unsigned)((lanes + 63) / 64)), scan_grid((unsigned)((G.n_rows + 1) / 2));
   hipLaunchKernelGGL(sos_transition_kernel<NS>, dim3(1), dim3(64), 0, st, sos, G.L, M);
   // forward pass over the odd extension -> y
-  hipLaunchKernelGGL((sos_block_kernel<T, NS, false, false>), grid, dim3(256), 0, st, x, y, G, sos, zi, S);
+  hipLaunchKernelGGL((sos_block_kernel<T, NS, false, false>), grid, dim3(64), 0, st, x, y, G, sos, zi, S);
   if (G.nb > 2) hipLaunchKernelGGL(sos_scan_kernel<NS>, scan_grid, dim3(64), 0, st, G, (const double*)M, S);
-  hipLaunchKernelGGL((sos_block_kernel<T, NS, false, true>), grid, dim3(256), 0, st, x, y, G, sos, zi, S);
+  hipLaunchKernelGGL((sos_block_kernel<T, NS, false, true>), grid, dim3(64), 0, st, x, y, G, sos, zi, S);
   // backward pass over reversed y -> the trimmed row
-  hipLaunchKernelGGL((sos_block_kernel<T, NS, true, false>), grid, dim3(256), 0, st, x, y, G, sos, zi, S);
+  hipLaunchKernelGGL((sos_block_kernel<T, NS, true, false>), grid, dim3(64), 0, st, x, y, G, sos, zi, S);
   if (G.nb > 2) hipLaunchKernelGGL(sos_scan_kernel<NS>, scan_grid, dim3(64), 0, st, G, (const double*)M, S);
-  hipLaunchKernelGGL((sos_block_kernel<T, NS, true, true>), grid, dim3(256), 0, st, x, y, G, sos, zi, S);
+  hipLaunchKernelGGL((sos_block_kernel<T, NS, true, true>), grid, dim3(64), 0, st, x, y, G, sos, zi, S);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
 }

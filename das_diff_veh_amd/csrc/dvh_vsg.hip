@@ -853,6 +853,126 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
   }
 }
 
+// ---- scan skipping (DVH_SCAN_SKIP): the scan leaves out the 1 KB blocks of a gather row that lie wholly inside
+// the row's correlated slices -- [a + q hop, + w) over its nwin sub-windows on each side, loaded by the
+// correlation waves, which report a NaN / inf among them to the pass's flag (FusedOps::report).  Only for the
+// default windows (window = pass) of the fused engines.  A window whose flag ends at 0 (nothing non-zero in
+// the scanned part) is rescanned whole afterwards (window_zero_fixup_kernel), so all-zero windows stay exact.
+constexpr int kBlkF = 256;  // floats per scan block: one 16-byte load per lane
+#ifndef DVH_SKIP_DEPTH
+#define DVH_SKIP_DEPTH 12
+#endif
+constexpr int kSkipDepth = DVH_SKIP_DEPTH;  // 16-byte loads per lane in flight in the skipping scan
+
+// the gather row's skipped block ranges [s0, e0), [s1, e1) (blocks wholly inside a correlated slice)
+__device__ __forceinline__ void row_skip(const VsgArgs& A, int p, int i, int& s0, int& e0, int& s1, int& e1) {
+  s0 = e0 = s1 = e1 = 0;
+  if (i < 0 || i >= A.R) return;
+  const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
+  auto range = [&](int a, int L, int& s, int& e) {
+    const int nw = n_subwin(L, A.w, A.hop);
+    const int cov = nw > 0 ? (nw - 1) * A.hop + A.w : 0;
+    s = (a + kBlkF - 1) / kBlkF;
+    e = (a + cov) / kBlkF;
+    if (e <= s) s = e = 0;
+  };
+  range(sld(seg), sld(seg + 1), s0, e0);
+  if (A.flags & kFlagOtherSide) range(sld(seg + 2), sld(seg + 3), s1, e1);
+  if (s1 < s0) {  // ordered
+    int t = s0; s0 = s1; s1 = t;
+    t = e0; e0 = e1; e1 = t;
+  }
+  if (e0 > s1 && s1 < e1) {  // overlapping ranges merge
+    e0 = max(e0, e1);
+    s1 = e1 = 0;
+  }
+}
+
+// rows [c0, c1) of pass p's window (n_t samples each, ch_stride apart, 16-byte aligned rows): max |x| bit
+// pattern over the blocks the correlation does not load; kScanDepth 16-byte loads per lane in flight, the
+// cursor (row, block, skip ranges) advanced in scalar registers
+__device__ __forceinline__ uint32_t scan_rows_skip(const VsgArgs& A, const ScanArgs& S, int p, int c0, int c1, int lane) {
+  const float* base = A.win + (int64_t)p * A.pass_stride;
+  const int64_t wbytes = ((int64_t)(S.n_ch - 1) * A.ch_stride + S.n_t) * 4;
+  const __amdgpu_buffer_rsrc_t rs = scan_rsrc(base, (uint32_t)min<int64_t>(wbytes, 0xffffffffLL));
+  const int row0 = sld(A.pass_tab + 2 * p);
+  const int nblk = (S.n_t + kBlkF - 1) / kBlkF;
+  int c = c0, j = 0, s0, e0, s1, e1;
+  row_skip(A, p, c - row0, s0, e0, s1, e1);
+  auto fix = [&]() {  // the cursor past the skipped ranges and onto the next row when a row is done
+    for (;;) {
+      if (j >= s0 && j < e0) j = e0;
+      if (j >= s1 && j < e1) j = e1;
+      if (j < nblk || c >= c1) return;
+      ++c;
+      j = 0;
+      if (c < c1) row_skip(A, p, c - row0, s0, e0, s1, e1);
+    }
+  };
+  fix();
+  const int lofs = lane * 16;
+  auto next = [&]() -> int {  // byte offset of this lane's 16 bytes of the cursor's block (out of range when done)
+    int off = -1;
+    if (c < c1) {
+      const int f = j * kBlkF + lane * 4;
+      off = f < S.n_t ? (int)(((int64_t)c * A.ch_stride + (int64_t)j * kBlkF) * 4) + lofs : -1;
+      ++j;
+      fix();
+    }
+    return off;
+  };
+  constexpr int D = kSkipDepth;
+  uint32_t m = 0;
+  u32x4 r[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, next(), 0, kScanAux);
+  while (c < c1) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const u32x4 v = r[d] & 0x7fffffffu;
+      m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, next(), 0, kScanAux);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const u32x4 v = r[d] & 0x7fffffffu;
+    m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+  }
+  return wave_max_u32(m);
+}
+
+// scan_units with skipping (default windows only: window s = pass order[q])
+__device__ __forceinline__ void scan_units_skip(const VsgArgs& A, const ScanArgs& S, uint32_t* __restrict__ vflag,
+                                                uint32_t* __restrict__ counter, int lane,
+                                                const int32_t* __restrict__ sorder) {
+  const int upp = (S.n_ch + kScanRows - 1) / kScanRows;
+  const int n_units = S.n_win * upp;
+  int u = pull_unit(counter, lane);
+  while (u < n_units) {
+    const int un = pull_unit(counter, lane);
+    const int q = u / upp, c0 = (u - q * upp) * kScanRows;
+    const int s = sorder ? sld(sorder + q) : q;
+    const uint32_t m = scan_rows_skip(A, S, s, c0, min(c0 + kScanRows, S.n_ch), lane);
+    if (lane == 0) atomicMax(vflag + s, m);
+    u = un;
+  }
+}
+
+// Windows whose flag is still 0 after a skipping launch are rescanned whole (their scanned part was all zero;
+// the correlated slices may not be): one block per window, nothing to do for the usual non-zero flag.
+__global__ __launch_bounds__(256) void window_zero_fixup_kernel(VsgArgs A, ScanArgs S, uint32_t* __restrict__ vflag) {
+  const int s = blockIdx.x;
+  if (vflag[s] != 0) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float* base = A.win + (int64_t)s * A.pass_stride;
+  uint32_t m = 0;
+  for (int c = wave; c < S.n_ch; c += 4)
+    for (int t = lane; t < S.n_t; t += 64) m = max(m, absbits(base[(int64_t)c * A.ch_stride + t]));
+  m = wave_max_u32(m);
+  if (lane == 0 && m) atomicMax(vflag + s, m);
+}
+
 #ifndef DVH_CORR_PRIO
 #define DVH_CORR_PRIO 2  // s_setprio of the correlation waves while they correlate (scan waves stay at 0): the
                          // correlation is the critical path; 1 / 2 / 3 all measured 127.7 k -> 136 k windows/s on synth10k
@@ -881,6 +1001,11 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
   E eng = make_engine<E>(lds);
   bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool skip = DVH_SCAN_SKIP && Fused<E>::v && !S.tab && S.n_t % 4 == 0 && A.ch_stride % 4 == 0 &&
+                    A.pass_stride % 4 == 0 && (reinterpret_cast<uintptr_t>(A.win) % 16 == 0);
+  if constexpr (Fused<E>::v) {
+    if (skip) eng.vflag = vflag;
+  }
   if (wave < kFft) {
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
@@ -893,7 +1018,8 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
   }
   // the chunks cover order[0, end of the last chunk): scan in that order when it lists every pass
   const int32_t* sorder = (n_chunk > 0 && sld(chunk_tab + 3 * (n_chunk - 1) + 1) == A.n_pass) ? order : nullptr;
-  scan_units(A, S, vflag, counter, lane, sorder);
+  if (skip) scan_units_skip(A, S, vflag, counter, lane, sorder);
+  else scan_units(A, S, vflag, counter, lane, sorder);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
@@ -1194,6 +1320,10 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
     const int grid = (int)(need < v.bpc * cu_count() ? (need > 0 ? need : 1) : v.bpc * cu_count());
     void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &tab};
     if (int rc = launch(v.fn, grid, v.fft + v.scan, v.lds, args, s)) return rc;
+    if (DVH_SCAN_SKIP && !scan_tab && S.n_win > 0) {  // the windows the skipping scan saw as all zero, rescanned whole
+      hipLaunchKernelGGL(window_zero_fixup_kernel, dim3((unsigned)S.n_win), dim3(256), 0, s, A, S, vflag);
+      if ((e = hipGetLastError()) != hipSuccess) return set_error(-3, hipGetErrorString(e));
+    }
   } else {  // no fused form: the scan as its own launch, then the plain stack launch
     void* sargs[] = {&A, (void*)&S, &vflag, &counter};
     if (int rc = launch((const void*)window_scan_kernel, 4 * cu_count(), 4, 0, sargs, s)) return rc;

@@ -112,6 +112,14 @@ __device__ __forceinline__ int opaque(int v) {
 
 // |x| != 0 as a bit mask (NaN included); OR-accumulate, test once per sub-window
 __device__ __forceinline__ uint32_t nzbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
+// the fused engines accumulate max |x| bit patterns instead (same cost): != 0 is the same non-zero test, and
+// >= 0x7f800000 flags a NaN / inf among the loaded samples (the validity of the bytes the scan leaves out)
+__device__ __forceinline__ uint32_t maxbits(uint32_t b, float x) { return max(b, nzbits(x)); }
+constexpr uint32_t kInfBits = 0x7f800000u;
+
+#ifndef DVH_SCAN_SKIP
+#define DVH_SCAN_SKIP 0  // validated launch: the scan skips the correlated slices, which the correlation validates
+#endif
 
 __device__ __forceinline__ void accumulate_cross(float2 Az, float2 Bc, float2& C) {
   // P = (A + B) / 2, R = (A - B) / 2i with B = conj(Bc)  ->  P conj(R) = (i / 4) (A + B) conj(A - B)
@@ -319,6 +327,7 @@ struct FusedOps {
   bool live_f, live_o;
   const float2* tab = nullptr;  // the pass table of pivot spectra (stack kernels), or none
   int w;                        // sub-window length: the padded engines load samples n < w
+  uint32_t* vflag = nullptr;    // validated launch with scan skipping: per-pass flags the loads report NaN / inf to
 
   __device__ FusedOps(char* lds, int wave, int lane_, int w_) : lane(lane_), live_f(false), live_o(false), w(w_) {
     tw = reinterpret_cast<float2*>(lds);
@@ -333,6 +342,11 @@ struct FusedOps {
   // the stages after stage 1 of the transform whose stage-1 output is in bufB; cross spectra into C
   __device__ __forceinline__ void finish(float2 (&C)[kNH]) const {
     self().finish_with([&](int j, float2 a, float2 b) { accumulate_cross(a, b, C[j]); });
+  }
+
+  // a NaN / inf among the samples this wave loaded for pass p (max |x| bits vm) -> the pass's validity flag
+  __device__ __forceinline__ void report(int p, uint32_t vm) const {
+    if (DVH_SCAN_SKIP && vflag && __ballot(vm >= kInfBits) != 0 && lane == 0) atomicMax(vflag + p, kInfBits);
   }
 
   // the pass's table entries hold all its sub-windows (head nwin of entry 0 >= 0)
@@ -353,14 +367,16 @@ struct FusedOps {
     live_f = live_o = false;
     auto start = [&](int q) { return q < t.nwin_f ? t.a_f + q * hop : t.a_o + (q - t.nwin_f) * hop; };
     float2 z[kNJ];
+    uint32_t vm = 0;
     if (nq > 0) load(t, start(0), z);
     for (int q = 0; q < nq; ++q) {
       uint32_t bp = 0, br = 0;
 #pragma unroll
       for (int j = 0; j < kNJ; ++j) {
-        bp |= nzbits(z[j].x);
-        br |= nzbits(z[j].y);
+        bp = maxbits(bp, z[j].x);
+        br = maxbits(br, z[j].y);
       }
+      if (DVH_SCAN_SKIP) vm = max(vm, max(bp, br));
       const bool live = (__ballot(bp != 0) != 0) && (__ballot(br != 0) != 0);
       if (live) self().stage1(z);
       if (q + 1 < nq) load(t, start(q + 1), z);
@@ -373,6 +389,7 @@ struct FusedOps {
         finish(Co);
       }
     }
+    report(t.p, vm);
   }
 
   // ---- spectra_tab: the sub-windows whose pivot slices the table holds cost only their receivers ----
@@ -430,15 +447,17 @@ struct FusedOps {
     const TabJobs J = tab_jobs(t, head);
     const int nj = J.npair + J.nt;
     float2 z[kNJ];
+    uint32_t vm = 0;
     if (nj > 0) tab_load(t, J, 0, hop, z);
     for (int k = 0; k < nj; ++k) {
       const bool pairjob = k < J.npair;
       uint32_t bp = 0, br = 0;
 #pragma unroll
       for (int j = 0; j < kNJ; ++j) {
-        bp |= nzbits(z[j].x);
-        br |= nzbits(z[j].y);
+        bp = maxbits(bp, z[j].x);
+        br = maxbits(br, z[j].y);
       }
+      if (DVH_SCAN_SKIP) vm = max(vm, max(bp, br));
       const bool nzp = __ballot(bp != 0) != 0, nzr = __ballot(br != 0) != 0;
       int s0 = 0, q0 = 0, a0 = 0, s1 = 0, q1 = 0, a1 = 0;
       bool la = false, lb = false;
@@ -499,6 +518,7 @@ struct FusedOps {
         finish(Co);
       }
     }
+    report(t.p, vm);
   }
 
   // ---- direct_task: a row task whose passes have only a table-served forward side ----
@@ -593,8 +613,12 @@ struct FusedOps {
       uint32_t bp = 0, br = 0;
 #pragma unroll
       for (int j = 0; j < kNJ; ++j) {
-        bp |= nzbits(z[j].x);
-        br |= nzbits(z[j].y);
+        bp = maxbits(bp, z[j].x);
+        br = maxbits(br, z[j].y);
+      }
+      if (DVH_SCAN_SKIP) {  // each half's samples belong to its own pass: halves 2 jb, 2 jb + 1 of W per pass
+        report(__builtin_amdgcn_readlane(p, (2 * jb) / W), bp);
+        if (hb) report(__builtin_amdgcn_readlane(p, (2 * jb + 1) / W), br);
       }
       // a receiver slice or its pivot slice identically zero: exactly zero in the reference
       const bool la = (__ballot(bp != 0) != 0) && sld(&Pa[BINS - 1].x) != 0.f;

@@ -15,7 +15,7 @@ def default_device():
 # by a thread pool into one of two pinned buffers (in the windows' own dtype, no host-side conversion), sent
 # by an asynchronous H2D copy on a side stream, and converted to float32 on the device, so that the host copy
 # of chunk k + 1 runs while chunk k crosses PCIe.
-STAGE_BYTES = 64 << 20
+STAGE_BYTES = 128 << 20
 _STAGE = {}
 
 
@@ -36,7 +36,7 @@ def _pool():
     import concurrent.futures as cf
     import os
     if "pool" not in _STAGE:
-        _STAGE["pool"] = cf.ThreadPoolExecutor(max(1, min(8, os.cpu_count() or 1)))
+        _STAGE["pool"] = cf.ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1)))
     return _STAGE["pool"]
 
 

@@ -46,9 +46,30 @@ def _shared_or_stacked(arrays):
     return np.stack([np.asarray(a, dtype=np.float64) for a in arrays])
 
 
+def _axes_all(windows, prm: VsgParams):
+    """_axes of every window, evaluated once per distinct (channel axis, dt): notebook windows of one fiber
+    section share their axes' values (the reference's per-window argmax searches give the same answer)."""
+    memo, keys, axes = {}, [], []
+    for w in windows:
+        x = np.asarray(w.x_axis, dtype=np.float64)
+        t = np.asarray(w.t_axis, dtype=np.float64)
+        mk = (x.tobytes(), t[:2].tobytes()) if t.size >= 2 else None
+        if mk is None or mk not in memo:
+            r = _axes(w, prm)
+            if mk is None:
+                keys.append(r[0])
+                axes.append(r[1])
+                continue
+            memo[mk] = r
+        k, a = memo[mk]
+        keys.append(k)
+        axes.append(GatherAxes(a.gather_x_axis.copy(), a.gather_t_axis.copy()))  # each image owns its axes
+    return keys, axes
+
+
 def group_windows(windows, prm: VsgParams, device):
     """[(indices, DevicePlan)] per (data shape, R, w, hop) group, and every pass's GatherAxes."""
-    keys, axes = zip(*[_axes(w, prm) for w in windows]) if windows else ((), ())
+    keys, axes = _axes_all(windows, prm) if windows else ((), ())
     groups = {}
     for i, (w, k) in enumerate(zip(windows, keys)):
         groups.setdefault((tuple(w.data.shape),) + k, []).append(i)

@@ -373,15 +373,21 @@ def pack_trajectories(trajectories, device):
     stable sort first, as interp1d does (its mergesort of the abscissae)."""
     import torch
     n = len(trajectories)
-    L = max(1, max(len(vx) for vx, _ in trajectories))
+    lens = np.array([len(vx) for vx, _ in trajectories], dtype=np.int64)
+    L = max(1, int(lens.max()) if n else 1)
     tx = np.zeros((n, L))
     tt = np.zeros((n, L))
-    ln = np.zeros(n, dtype=np.int32)
-    for i, (vx, vt) in enumerate(trajectories):
-        vx, vt = np.asarray(vx, dtype=np.float64), np.asarray(vt, dtype=np.float64)
-        o = np.argsort(vx, kind="mergesort")
-        k = len(vx)
-        tx[i, :k], tt[i, :k], ln[i] = vx[o], vt[o], k
+    ln = lens.astype(np.int32)
+    # trajectories of one length are ordered together: a row-wise stable argsort equals each row's mergesort,
+    # and rows already ascending (the tracker's output) are copied as they are
+    for k in np.unique(lens):
+        idx = np.flatnonzero(lens == k)
+        vx = np.array([np.asarray(trajectories[i][0], dtype=np.float64) for i in idx]).reshape(idx.size, k)
+        vt = np.array([np.asarray(trajectories[i][1], dtype=np.float64) for i in idx]).reshape(idx.size, k)
+        if k > 1 and not np.all(vx[:, 1:] > vx[:, :-1]):
+            o = np.argsort(vx, axis=1, kind="stable")
+            vx, vt = np.take_along_axis(vx, o, 1), np.take_along_axis(vt, o, 1)
+        tx[idx, :k], tt[idx, :k] = vx, vt
     return (torch.from_numpy(tx).to(device), torch.from_numpy(tt).to(device), torch.from_numpy(ln).to(device))
 
 

@@ -27,6 +27,12 @@ extern "C" {
 int dvh_abi_version(void);
 const char* dvh_last_error(void);
 
+/* Host function: `times` successive random.sample(range(lo, lo + n), k) draws of CPython's `random`
+ * (bootstrap_disp's draws, apis/imaging_classes.py:8-48), bit for bit, from the Mersenne Twister state
+ * random.getstate()[1] (624 words + index, uint32[625], updated in place for random.setstate()).
+ * out: int64 [times][k] (host memory). */
+int dvh_random_sample(uint32_t* state, int64_t lo, int64_t n, int32_t k, int32_t times, int64_t* out);
+
 /* ---------------------------------------------------------------- virtual shot gathers
  * pass_tab [n_pass][2] = {row0 (= start_idx), pivot_idx};  gather row i is channel row0 + i.
  * seg_tab  [n_pass][R][2 sides][2] = {slice start, slice length} of the row's time slice on the

@@ -410,3 +410,28 @@ def test_fv_mfma_tables_reproduce_interp2d(nv, nf):
         assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max(), f
     assert np.array_equal(cb // plan.n_fb, plan.mk)
     assert np.all(cb % plan.n_fb == plan.fj[:, None])
+
+
+def test_native_draws_equal_python_random_sample():
+    """bootstrap.draw forms random.sample(range(1, n), k) draws in the library (dvh_random_sample) from the
+    generator's Mersenne Twister state: bit-identical to Python's own calls for the set (n > setsize) and pool
+    (small n) branches, k = 0 .. 60, and the generator continues exactly where Python's calls leave it."""
+    import random
+
+    from das_diff_veh_amd import bootstrap as bt
+    for n, ks, times in ((1442, range(0, 61), 30), (7, range(0, 7), 5), (30, (1, 5, 6, 20, 29), 4),
+                         (100, (6, 33, 99), 3), (2, (0, 1), 4)):
+        for k in ks:
+            ra, rb = random.Random(1234 + n + k), random.Random(1234 + n + k)
+            got = bt.draw(n, k, times, rand=ra)
+            ref = np.array([rb.sample(range(1, n), k) for _ in range(times)], dtype=np.int32).reshape(times, k)
+            assert np.array_equal(got, ref), (n, k)
+            assert ra.random() == rb.random() and ra.getrandbits(64) == rb.getrandbits(64), (n, k)
+    # the module-level generator (the reference's random.seed / random.sample)
+    random.seed(7)
+    got = bt.draw(1442, 60, 30)
+    random.seed(7)
+    ref = np.array([random.sample(range(1, 1442), 60) for _ in range(30)], dtype=np.int32)
+    assert np.array_equal(got, ref)
+    with pytest.raises(ValueError):
+        bt.draw(5, 5, 1)
