@@ -24,6 +24,13 @@ namespace dvh {
 
 constexpr int kMaxSec = 16;
 
+// orders one wave's LDS stores and loads (a single-wave block: the fence keeps the compiler from moving them)
+__device__ __forceinline__ void wave_barrier_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------------------------------------
 // sosfiltfilt, time-parallel.  The cascade of n_sec transposed-direct-form-II sections (scipy's sosfilt:
 // o = b0 v + z0; z0 = b1 v - a1 o + z1; z1 = b2 v - a2 o) is linear in its 2 n_sec states, so a sequence
@@ -199,29 +206,33 @@ __global__ __launch_bounds__(64) void sos_block_kernel(T* __restrict__ x, double
     if (j < 0) return 2.0 * (double)row[0] - (double)row[-j];                    // i < padlen
     return 2.0 * (double)row[G.n_t - 1] - (double)row[2 * (G.n_t - 1) - j];     // past the end
   };
-  for (int64_t ch = 0; ch < n_chunks; ++ch) {
-    const int64_t cbase = ch * kSosCh;
-    // cooperative load: run s's samples [i0_s + cbase, + kSosCh)
-    {
-      int64_t rs = r_l;
-      int ks = k_l;
-#pragma unroll 4
-      for (int m = 0; m < 16; ++m) {
-        const int sidx = 4 * m + l4;
-        double v = 0.0;
-        if (g0 + sidx < n_lanes) {
-          const int64_t i = (int64_t)ks * G.L + cbase + e;
-          if (i < min((int64_t)(ks + 1) * G.L, G.n_ext)) v = in_at(rs, i);
-        }
-        tile[sidx * kSosLd + e] = v;
-        ks += 4;
-        while (ks >= G.nb) {
-          ks -= G.nb;
-          ++rs;
-        }
+  // cooperative load of chunk ch into registers (this lane's 16 values: runs 4 m + l4, sample e)
+  double pv[16];
+  auto coop_load = [&](int64_t cbase) {
+    int64_t rs = r_l;
+    int ks = k_l;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      double v = 0.0;
+      if (g0 + 4 * m + l4 < n_lanes) {
+        const int64_t i = (int64_t)ks * G.L + cbase + e;
+        if (i < min((int64_t)(ks + 1) * G.L, G.n_ext)) v = in_at(rs, i);
+      }
+      pv[m] = v;
+      ks += 4;
+      while (ks >= G.nb) {
+        ks -= G.nb;
+        ++rs;
       }
     }
+  };
+  if (n_chunks > 0) coop_load(0);
+  for (int64_t ch = 0; ch < n_chunks; ++ch) {
+    const int64_t cbase = ch * kSosCh;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) tile[(4 * m + l4) * kSosLd + e] = pv[m];
     __syncthreads();
+    if (ch + 1 < n_chunks) coop_load(cbase + kSosCh);  // the next chunk's loads in flight under this one's recursion
     const int64_t nn = min((int64_t)kSosCh, i1 - i0 - cbase);
     if (OUT) {
       for (int t = 0; t < nn; ++t) tile[lane * kSosLd + t] = c.step(z0, z1, tile[lane * kSosLd + t]);
@@ -267,10 +278,13 @@ __global__ __launch_bounds__(64) void sos_block_kernel(T* __restrict__ x, double
 }
 
 // Phase B: s_k = e_k + M s_{k-1} for k = 1 .. nb - 2 (s_0 = e_0 is already the true state).  Two rows per
-// wave (lanes 0-31 / 32-63), lane j = state component j.
+// wave (lanes 0-31 / 32-63), lane j = state component j.  Each step's state goes through LDS: one 8-byte store
+// per lane, then every lane reads the half's whole state with broadcast 16-byte reads (no per-element
+// cross-lane shuffles on the step's critical path).
 template <int NS>
 __global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* __restrict__ M, double* __restrict__ S) {
   constexpr int NST = 2 * NS;
+  __shared__ __attribute__((aligned(16))) double sv[2][32];
   const int half = threadIdx.x >> 5, j = threadIdx.x & 31;
   const int64_t r = 2 * (int64_t)blockIdx.x + half;
   const bool act = r < G.n_rows && j < NST;
@@ -278,8 +292,7 @@ __global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* _
 #pragma unroll
   for (int i = 0; i < NST; ++i) m[i] = act ? M[j * NST + i] : 0.0;
   double* Sr = S + (act ? r : 0) * (int64_t)G.nb * NST;
-  double s = act ? Sr[j] : 0.0;
-  const int base = half * 32;
+  sv[half][j] = act ? Sr[j] : 0.0;
   // the zero-state end states e_k come from memory 8 steps at a time, the next 8 loaded under this group's
   // arithmetic (a load per step would put one memory latency on the critical path of every step)
   constexpr int PF = 8;
@@ -297,13 +310,23 @@ __global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* _
     for (int t = 0; t < PF; ++t) {
       const int k = kb + t;
       if (k < kend) {
+        wave_barrier_lds();
+        const double2* v2 = reinterpret_cast<const double2*>(sv[half]);
+        double x[NST];
+#pragma unroll
+        for (int i = 0; i < NST / 2; ++i) {
+          const double2 u = v2[i];
+          x[2 * i] = u.x;
+          x[2 * i + 1] = u.y;
+        }
         // M s in four partial sums (a 5-deep instead of a 20-deep chain of dependent FMAs per step)
         double pa[4] = {cur[t], 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int i = 0; i < NST; ++i) pa[i & 3] += m[i] * __shfl(s, base + i);
+        for (int i = 0; i < NST; ++i) pa[i & 3] += m[i] * x[i];
         const double acc = (pa[0] + pa[1]) + (pa[2] + pa[3]);
         if (act) Sr[(int64_t)k * NST + j] = acc;
-        s = acc;
+        wave_barrier_lds();
+        sv[half][j] = acc;
       }
     }
 #pragma unroll

@@ -115,6 +115,17 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// the next index from a global work counter (one atomic per wave)
+__device__ __forceinline__ int pull_unit(uint32_t* counter, int lane) {
+  int u = 0;
+  if (lane == 0) u = (int)atomicAdd(counter, 1u);
+  return __builtin_amdgcn_readfirstlane(__shfl(u, 0));
+}
+
+#ifndef DVH_PULL_TASKS
+#define DVH_PULL_TASKS 0  // validated launch: correlation waves pull row tasks from a counter (A/B; static stride else)
+#endif
+
 // XCD-aware block order (blocks are dealt round robin over the 8 XCDs, each with its own L2):
 // consecutive logical blocks -- the row tasks of one pass chunk, which all read that chunk's pivot
 // channel -- run on the same XCD.  A bijection on [0, gridDim.x).
@@ -393,7 +404,8 @@ template <class E>
 __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
-                                             float* __restrict__ stack, int64_t t0, int64_t stride) {
+                                             float* __restrict__ stack, int64_t t0, int64_t stride,
+                                             uint32_t* tq = nullptr) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -402,7 +414,12 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
   const bool norm = (A.flags & kFlagNorm) != 0;
   const int h = N / 2;
   const int64_t n_task = (int64_t)n_chunk * A.R;
-  for (int64_t t = t0; t < n_task; t += stride) {
+  // tasks t0, t0 + stride, ... (static), or pulled from the counter tq; the next index fetched at the top of
+  // the task so that `continue` moves on
+  const int lane_t = threadIdx.x & 63;
+  int64_t tn = tq ? pull_unit(tq, lane_t) : t0;
+  for (int64_t t = tn; t < n_task; t = tn) {
+    tn = tq ? (int64_t)pull_unit(tq, lane_t) : t + stride;
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
     int np = -1, ni = 0;
@@ -537,7 +554,8 @@ template <class E>
 __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
-                                             float* __restrict__ stack, int64_t t0, int64_t stride) {
+                                             float* __restrict__ stack, int64_t t0, int64_t stride,
+                                             uint32_t* tq = nullptr) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -546,7 +564,12 @@ __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const flo
   const bool norm = (A.flags & kFlagNorm) != 0;
   const int w = A.w, h = w / 2;
   const int64_t n_task = (int64_t)n_chunk * A.R;
-  for (int64_t t = t0; t < n_task; t += stride) {
+  // tasks t0, t0 + stride, ... (static), or pulled from the counter tq; the next index fetched at the top of
+  // the task so that `continue` moves on
+  const int lane_t = threadIdx.x & 63;
+  int64_t tn = tq ? pull_unit(tq, lane_t) : t0;
+  for (int64_t t = tn; t < n_task; t = tn) {
+    tn = tq ? (int64_t)pull_unit(tq, lane_t) : t + stride;
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
     float* o = stack + ((int64_t)slot * A.R + i) * A.w;
@@ -765,15 +788,14 @@ constexpr int kScanRows = 16;
 #define DVH_SCAN_DEPTH 16
 #endif
 constexpr int kScanDepth = DVH_SCAN_DEPTH;  // 16-byte loads per lane in flight
-constexpr int kScanAux = 2;  // cache policy of the scan's buffer loads (nt; allocating loads measured 4 % slower)
+#ifndef DVH_SCAN_AUX
+#define DVH_SCAN_AUX 2
+#endif
+constexpr int kScanAux = DVH_SCAN_AUX;  // cache policy of the scan's buffer loads (nt; allocating loads measured 4 %
+                                        // slower on synth10k)
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
 
-__device__ __forceinline__ int pull_unit(uint32_t* counter, int lane) {
-  int u = 0;
-  if (lane == 0) u = (int)atomicAdd(counter, 1u);
-  return __builtin_amdgcn_readfirstlane(__shfl(u, 0));
-}
 
 // Buffer descriptor over [p, p + bytes) built from wave-uniform values (no waterfall loops around the
 // loads); out-of-range loads return 0, which leaves a max |x| unchanged.
@@ -984,9 +1006,9 @@ template <class E, bool EXACT>
 __device__ __forceinline__ void stack_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                             const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                             int32_t n_chunk, const float* __restrict__ weight, float* __restrict__ stack,
-                                            int64_t t0, int64_t stride) {
-  if constexpr (EXACT) stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride);
-  else stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride);
+                                            int64_t t0, int64_t stride, uint32_t* tq) {
+  if constexpr (EXACT) stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq);
+  else stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq);
 }
 
 // Persistent validated stack launch: blocks of kFft correlation waves + kScan scan waves (EngF500: two per CU;
@@ -1011,7 +1033,7 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
 #endif
     stack_tasks<E, EXACT>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
-                          (int64_t)gridDim.x * kFft);
+                          (int64_t)gridDim.x * kFft, DVH_PULL_TASKS ? counter + 1 : nullptr);
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1309,7 +1331,7 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   uint32_t* vflag = work;
   uint32_t* counter = work + S.n_win;
   float2* tab = (table_engine(n) && spec_ws) ? reinterpret_cast<float2*>(spec_ws) : nullptr;
-  hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t) * ((size_t)S.n_win + 1), s);
+  hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t) * ((size_t)S.n_win + 2), s);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
   if (tab)
     if (int rc = launch_table(A, n, tab, s)) return rc;

@@ -32,11 +32,16 @@ def _stager(device, dtype, nbytes):
     return st
 
 
+import os  # noqa: E402
+
+_NTHREADS = max(1, min(16, os.cpu_count() or 1))
+STAGE_MODE = os.environ.get("DVH_STAGE_MODE", "pool")  # pool | torch (A/B of the host copy into pinned memory)
+
+
 def _pool():
     import concurrent.futures as cf
-    import os
     if "pool" not in _STAGE:
-        _STAGE["pool"] = cf.ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1)))
+        _STAGE["pool"] = cf.ThreadPoolExecutor(_NTHREADS)
     return _STAGE["pool"]
 
 
@@ -61,8 +66,18 @@ def stage_windows(hosts, device, out=None):
         kk = min(k, n - a)
         b = ci & 1
         st["free"][b].synchronize()  # the H2D that last read this pinned buffer is done
-        view = st["pinned"][b].numpy()[:kk * per].view(src).reshape((kk,) + tuple(shape))
-        list(pool.map(lambda j: np.copyto(view[j], hosts[a + j], casting="unsafe"), range(kk)))
+        if STAGE_MODE == "torch":  # torch's parallel CPU cat into the pinned buffer
+            pin_t = st["pinned"][b][:kk * per].view(tdt).view((kk,) + tuple(shape))
+            torch.stack([torch.from_numpy(np.ascontiguousarray(h, dtype=src)) for h in hosts[a:a + kk]], out=pin_t)
+        else:  # thread pool, contiguous runs of windows per task
+            view = st["pinned"][b].numpy()[:kk * per].view(src).reshape((kk,) + tuple(shape))
+            nt = min(kk, _NTHREADS)
+            bounds = [kk * q // nt for q in range(nt + 1)]
+
+            def run(q):
+                for j in range(bounds[q], bounds[q + 1]):
+                    np.copyto(view[j], hosts[a + j], casting="unsafe")
+            list(pool.map(run, range(nt)))
         with torch.cuda.stream(st["stream"]):
             pin = st["pinned"][b][:kk * per].view(tdt).view((kk,) + tuple(shape))
             if src == np.float32:

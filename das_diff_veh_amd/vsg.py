@@ -166,7 +166,7 @@ def vsg_stack_validated(windows: torch.Tensor, plan: VsgPlan, schedule: StackSch
     pass whose window has a NaN / inf or is all zero becomes NaN -- the reference's data / ||data||_F
     (apis/virtual_shot_gather.py:125) -- without a separate ||window||_F pass.  Needs norm or norm_amp
     (the raw mode's scale is ||data||_F itself: use window_sumsq + vsg_stack).  ``work`` (optional):
-    int32 device buffer of >= n_window + 1 elements, reused across calls.  ``scan``: the windows of a
+    int32 device buffer of >= n_window + 2 elements, reused across calls.  ``scan``: the windows of a
     unit launch (UnitScan; default: one window per pass)."""
     _check_windows(windows, plan)
     if not (plan.flags & 6):
@@ -187,8 +187,8 @@ def vsg_stack_validated(windows: torch.Tensor, plan: VsgPlan, schedule: StackSch
     if scales is None:
         scales = vsg_scales(windows, plan, validity=False)
     n_win = plan.n_pass if scan is None else scan.n_win
-    if work is None or work.numel() < n_win + 1 or work.dtype != torch.int32:
-        work = torch.empty(n_win + 1, dtype=torch.int32, device=windows.device)
+    if work is None or work.numel() < n_win + 2 or work.dtype != torch.int32:
+        work = torch.empty(n_win + 2, dtype=torch.int32, device=windows.device)
     stab, uscan = (None, None) if scan is None else scan.device_tables(windows.device)
     ws = spectra_workspace(plan, windows.device, getattr(plan, "_ws", None))
     _lib.call("dvh_vsg_stack_validated", _lib.ptr(windows), windows.stride(0), windows.stride(1), plan.n_pass,

@@ -102,8 +102,8 @@ int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stride, int3
  * launch (pass stride 0 over one flattened record, each (pass, pivot) unit a "pass") gives instead
  * n_scan windows of n_ch rows starting at record rows scan_tab[s], and unit_scan[p] = the window
  * whose validity unit p takes (a pass imaged at several pivots is read once).  work: device
- * workspace of (scan_tab ? n_scan : n_pass) + 1 uint32 (per-window max |x| bit pattern, a work
- * counter), zeroed inside. */
+ * workspace of (scan_tab ? n_scan : n_pass) + 2 uint32 (per-window max |x| bit pattern, two work
+ * counters), zeroed inside. */
 int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass, int32_t n_ch,
                             int32_t n_t, const int32_t* pass_tab, const int32_t* seg_tab, int32_t R, int32_t w,
                             int32_t hop, int32_t flags, const float* scales, const int32_t* order,

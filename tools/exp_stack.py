@@ -38,7 +38,11 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="fused,corr7,corr,sumsq")
     ap.add_argument("--workload", default="synth10k", choices=("synth10k", "weights", "speeds"))
+    ap.add_argument("--w499", action="store_true", help="time axes with w = 499 (zero-padded 1 024-point engine)")
     args = ap.parse_args()
+    if args.w499:
+        from das_diff_veh_amd.synth import DT_W499
+        bench.WORKLOADS[args.workload]["t0"] = DT_W499
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     job = bench.build(args.workload, dev, 1, 0)
