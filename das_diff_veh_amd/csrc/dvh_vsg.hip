@@ -919,8 +919,9 @@ __device__ __forceinline__ uint32_t scan_rows_skip(const VsgArgs& A, const ScanA
   const __amdgpu_buffer_rsrc_t rs = scan_rsrc(base, (uint32_t)min<int64_t>(wbytes, 0xffffffffLL));
   const int row0 = sld(A.pass_tab + 2 * p);
   const int nblk = (S.n_t + kBlkF - 1) / kBlkF;
-  int c = c0, j = 0, s0, e0, s1, e1;
+  int c = c0, j = 0, s0, e0, s1, e1, ns0, ne0, ns1, ne1;
   row_skip(A, p, c - row0, s0, e0, s1, e1);
+  row_skip(A, p, c + 1 - row0, ns0, ne0, ns1, ne1);  // the next row's ranges formed a row ahead
   auto fix = [&]() {  // the cursor past the skipped ranges and onto the next row when a row is done
     for (;;) {
       if (j >= s0 && j < e0) j = e0;
@@ -928,7 +929,11 @@ __device__ __forceinline__ uint32_t scan_rows_skip(const VsgArgs& A, const ScanA
       if (j < nblk || c >= c1) return;
       ++c;
       j = 0;
-      if (c < c1) row_skip(A, p, c - row0, s0, e0, s1, e1);
+      s0 = ns0;
+      e0 = ne0;
+      s1 = ns1;
+      e1 = ne1;
+      if (c + 1 < c1) row_skip(A, p, c + 1 - row0, ns0, ne0, ns1, ne1);
     }
   };
   fix();

@@ -112,14 +112,20 @@ __device__ __forceinline__ int opaque(int v) {
 
 // |x| != 0 as a bit mask (NaN included); OR-accumulate, test once per sub-window
 __device__ __forceinline__ uint32_t nzbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
-// the fused engines accumulate max |x| bit patterns instead (same cost): != 0 is the same non-zero test, and
-// >= 0x7f800000 flags a NaN / inf among the loaded samples (the validity of the bytes the scan leaves out)
-__device__ __forceinline__ uint32_t maxbits(uint32_t b, float x) { return max(b, nzbits(x)); }
-constexpr uint32_t kInfBits = 0x7f800000u;
-
 #ifndef DVH_SCAN_SKIP
 #define DVH_SCAN_SKIP 0  // validated launch: the scan skips the correlated slices, which the correlation validates
 #endif
+// With scan skipping the fused engines accumulate max |x| bit patterns (!= 0 is the same non-zero test, and
+// >= 0x7f800000 flags a NaN / inf among the loaded samples, the validity of the bytes the scan leaves out);
+// otherwise the OR (one v_and_or per sample against an and + max).
+__device__ __forceinline__ uint32_t maxbits(uint32_t b, float x) {
+#if DVH_SCAN_SKIP
+  return max(b, nzbits(x));
+#else
+  return b | nzbits(x);
+#endif
+}
+constexpr uint32_t kInfBits = 0x7f800000u;
 
 __device__ __forceinline__ void accumulate_cross(float2 Az, float2 Bc, float2& C) {
   // P = (A + B) / 2, R = (A - B) / 2i with B = conj(Bc)  ->  P conj(R) = (i / 4) (A + B) conj(A - B)

@@ -45,11 +45,12 @@ def _pool():
     return _STAGE["pool"]
 
 
-def stage_windows(hosts, device, out=None):
+def stage_windows(hosts, device, out=None, wait=True):
     """Same-shape 2-D NumPy arrays -> one float32 device tensor [n, C, T] (or into ``out``), pipelined:
     pinned double buffering, thread-parallel host copies, asynchronous H2D on a side stream, float64 ->
-    float32 conversion on the device.  The current stream waits for the copies; the call returns when the
-    last host copy is done (the caller's arrays are free to change afterwards)."""
+    float32 conversion on the device.  wait=True: the current stream waits for the copies; wait=False: the
+    caller waits on the returned event (stage_async).  The call returns when the last host copy is done (the
+    caller's arrays are free to change afterwards)."""
     n = len(hosts)
     shape = hosts[0].shape
     if any(h.shape != shape for h in hosts):
@@ -87,8 +88,29 @@ def stage_windows(hosts, device, out=None):
                 d.copy_(pin, non_blocking=True)
                 out[a:a + kk].copy_(d)
             st["free"][b].record(st["stream"])
-    torch.cuda.current_stream(device).wait_stream(st["stream"])
-    return out
+    done = torch.cuda.Event()
+    done.record(st["stream"])
+    if wait:
+        torch.cuda.current_stream(device).wait_event(done)
+        return out
+    return out, done
+
+
+def stage_async(hosts, device):
+    """stage_windows on a background thread: the host copies overlap the caller's own host work (e.g. the batch's
+    tables).  Returns a function that yields the device tensor, the current stream made to wait for it."""
+    import concurrent.futures as cf
+    if "bg" not in _STAGE:
+        _STAGE["bg"] = cf.ThreadPoolExecutor(1)
+    n = len(hosts)
+    out = torch.empty((n,) + tuple(hosts[0].shape), dtype=torch.float32, device=device)  # caller's stream
+    fut = _STAGE["bg"].submit(stage_windows, hosts, device, out, False)
+
+    def result():
+        t, ev = fut.result()
+        torch.cuda.current_stream(device).wait_event(ev)
+        return t
+    return result
 
 
 def to_device_f32(arrays, device=None):

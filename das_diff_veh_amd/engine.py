@@ -67,20 +67,41 @@ def _axes_all(windows, prm: VsgParams):
     return keys, axes
 
 
-def group_windows(windows, prm: VsgParams, device):
-    """[(indices, DevicePlan)] per (data shape, R, w, hop) group, and every pass's GatherAxes."""
+def _groups(windows, prm: VsgParams):
+    """{(data shape, R, w, hop): window indices} and every pass's GatherAxes (host only)."""
     keys, axes = _axes_all(windows, prm) if windows else ((), ())
     groups = {}
     for i, (w, k) in enumerate(zip(windows, keys)):
         groups.setdefault((tuple(w.data.shape),) + k, []).append(i)
-    out = []
-    for key, idx in groups.items():
-        ws = [windows[i] for i in idx]
-        trk = pack_trajectories([(w.veh_state_x, w.veh_state_t) for w in ws], device)
-        plan = DevicePlan(_shared_or_stacked([w.x_axis for w in ws]), _shared_or_stacked([w.t_axis for w in ws]),
-                          *trk, prm, key[0][0])
-        out.append((idx, plan.check()))
-    return out, list(axes)
+    return groups, list(axes)
+
+
+def _plan(windows, idx, key, prm: VsgParams, device):
+    ws = [windows[i] for i in idx]
+    trk = pack_trajectories([(w.veh_state_x, w.veh_state_t) for w in ws], device)
+    plan = DevicePlan(_shared_or_stacked([w.x_axis for w in ws]), _shared_or_stacked([w.t_axis for w in ws]),
+                      *trk, prm, key[0][0])
+    return plan.check()
+
+
+def group_windows(windows, prm: VsgParams, device):
+    """[(indices, DevicePlan)] per (data shape, R, w, hop) group, and every pass's GatherAxes."""
+    groups, axes = _groups(windows, prm)
+    return [(idx, _plan(windows, idx, key, prm, device)) for key, idx in groups.items()], axes
+
+
+def _stage(windows, idx, device):
+    """The group's windows to the device: host arrays through the pipelined staging on a background thread
+    (their copies overlap the group's table work), device tensors stacked directly.  Returns a callable."""
+    import torch
+
+    from .device import stage_async
+    arrs = [windows[i].data for i in idx]
+    if not any(isinstance(a, torch.Tensor) for a in arrs):
+        hosts = [np.asarray(a) for a in arrs]
+        if all(h.dtype in (np.float32, np.float64) and h.ndim == 2 for h in hosts):
+            return stage_async(hosts, device)
+    return lambda: to_device_f32(arrs, device)
 
 
 def gathers(windows, prm: VsgParams, device=None):
@@ -103,13 +124,15 @@ def stacked(windows, prm: VsgParams, slots=None, n_slot=1, device=None, chunk=8,
     device = device or default_device()
     slots = np.zeros(len(windows), dtype=np.int64) if slots is None else np.asarray(slots)
     counts = np.bincount(slots, minlength=n_slot) if counts is None else np.asarray(counts)
-    groups, axes = group_windows(windows, prm, device)
-    keys = {(plan.R, plan.w) for _, plan in groups}
-    if len(keys) != 1:
+    groups, axes = _groups(windows, prm)
+    if len({key[1:3] for key in groups}) != 1:
         raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
+    # every group's window copies start first (background thread), the tables are formed meanwhile
+    staged = [(idx, key, _stage(windows, idx, device)) for key, idx in groups.items()]
     out = None
-    for idx, plan in groups:
-        data = to_device_f32([windows[i].data for i in idx], device)
+    for idx, key, data_fn in staged:
+        plan = _plan(windows, idx, key, prm, device)
+        data = data_fn()
         sched = StackSchedule(slots[idx], n_slot, chunk=chunk, counts=counts)
         fn = vsg_stack_validated if plan.flags & 6 else vsg_stack
         out = fn(data, plan, sched, out=out, accumulate=out is not None)

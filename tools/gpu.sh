@@ -9,8 +9,10 @@
 #   bash tools/gpu.sh prof TAG [workload]        rocprofv3 --kernel-trace --stats of the bench ->
 #                                                gpurun_out/prof_TAG*/ (copy the stats CSV to profiles/)
 #   bash tools/gpu.sh pmc TAG [workload]         PMC passes -> profiles/TAG_pmc_summary[_workload].json
-#   bash tools/gpu.sh final TAG                  end of round: tests + smoke, PMC, bench line with the CPU
-#                                                baseline, kernel stats, for synth10k, sliding and timelapse
+#   bash tools/gpu.sh final TAG                  end of round: tests + smoke, PMC (synth10k, sliding, weights,
+#                                                timelapse), then `lines`
+#   bash tools/gpu.sh lines TAG                  every bench line with its CPU baseline (synth10k, weights, sliding,
+#                                                timelapse, w = 499, prep, bootstrap, speeds-host) + kernel stats
 set -o pipefail
 mode=${1:-tests}; shift
 mkdir -p gpurun_out
@@ -68,15 +70,31 @@ case $mode in
   final)
     tag=$1
     run_tests || exit 1
-    for wl in synth10k sliding; do
+    for wl in synth10k sliding weights; do
       bash "$0" pmc $tag $wl || exit 1
     done
     bash tools/pmc_timelapse.sh $tag > gpurun_out/pmc_tl.log 2>&1 || { echo pmc tl failed; tail -5 gpurun_out/pmc_tl.log; exit 1; }
+    bash "$0" lines $tag || exit 1
+    rm -rf gpurun_out/pmc_${tag}* ;;
+  lines)
+    tag=$1
     bench_line gpurun_out/${tag}_bench.json || exit 1
+    bench_line gpurun_out/${tag}_bench_weights.json --workload weights || exit 1
     bench_line gpurun_out/${tag}_bench_sliding.json --workload sliding --steps 4 --warmup 1 || exit 1
     bench_line gpurun_out/${tag}_bench_timelapse.json --workload timelapse || exit 1
-    for wl in synth10k sliding timelapse; do bash "$0" prof $tag $wl || exit 1; done
-    rm -rf gpurun_out/pmc_${tag}* ;;
+    bench_line gpurun_out/${tag}_bench_w499.json --w499 || exit 1
+    bench_line gpurun_out/${tag}_bench_prep.json --workload prep --steps 20 --warmup 3 || exit 1
+    bench_line gpurun_out/${tag}_bench_bootstrap.json --workload bootstrap --steps 5 --warmup 1 || exit 1
+    bench_line gpurun_out/${tag}_bench_speeds_host.json --workload speeds-host --steps 3 --warmup 1 || exit 1
+    for wl in synth10k weights sliding timelapse prep bootstrap; do bash "$0" prof $tag $wl || exit 1; done
+    bash "$0" profw499 $tag || exit 1 ;;
+  profw499)
+    tag=$1
+    prof_env
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${tag}_w499 -o ${tag}_w499 --output-format csv \
+      -- python bench.py --w499 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof_${tag}_w499.json \
+      2> gpurun_out/prof_${tag}_w499.err || { tail -5 gpurun_out/prof_${tag}_w499.err; exit 1; }
+    find gpurun_out/prof_${tag}_w499 -name '*kernel_trace.csv' -delete ;;
   *)
     echo "unknown mode $mode"; exit 2 ;;
 esac
