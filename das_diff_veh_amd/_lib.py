@@ -22,6 +22,7 @@ SIGNATURES = {
     "dvh_last_error": [],
     "dvh_vsg_fft_length": [_i32],
     "dvh_random_sample": [_p, _i64, _i64, _i32, _i32, _p],
+    "dvh_host_gather": [_p, _p, _i64, _i32],
     "dvh_window_sumsq": [_p, _i64, _i64, _i32, _i32, _i32, _p, _p],
     "dvh_pass_geometry": [_p, _i64, _p, _i64, _i32, _p, _p, _i64, _p, _p, _p, _i32, _i32, _f64, _i32, _i32, _p,
                           _p, _p],

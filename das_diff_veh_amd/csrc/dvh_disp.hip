@@ -763,6 +763,10 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 #ifndef DVH_FV_MF_GI
 #define DVH_FV_MF_GI 2  // images per wave in lock step (1 or 2)
 #endif
+#ifndef DVH_FV_MF_LATE
+#define DVH_FV_MF_LATE 0  // 1: a tile's table loads issued after the previous ones are consumed (half the
+                          // in-flight registers, a shorter load-to-use distance)
+#endif
 #ifndef DVH_FV_MF_WPE
 #define DVH_FV_MF_WPE (DVH_FV_MF_GI == 1 ? 3 : 2)  // waves per SIMD the kernel is register-budgeted for
 #endif
@@ -805,7 +809,14 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
   double* fks = smem;                   // [GI][nbuf]
   double* sgs = smem + GI * nbuf;       // taps + edge fits (L * L)
   double* bpad = sgs + L * L;           // [64]: taps at 16 .. 40, zeros around (the interior band)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // the lane index formed afresh where it is used (mbcnt of an opaque zero: no value kept live, or spilled,
+  // across the image loop)
+  auto lane_now = []() {
+    unsigned z = 0;
+    asm volatile("" : "+v"(z));
+    return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, z));
+  };
   // block -> (velocity block, image group); XCD-aware when the velocity blocks split evenly over the 8
   // XCDs (blocks are dealt round robin): every block of a velocity block then runs on one XCD and its
   // (f, v) table slice stays in that XCD's L2
@@ -822,14 +833,14 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
     }
   }
   const int b0 = ig * G, n_img = min(G, B - b0);
-  const int vw = vb * (kMfWaves * kMfV) + wave * kMfV;  // the wave's first velocity
-  const int li = lane & 15, kk = lane >> 4;
+  const int vw = vb * (kMfWaves * kMfV) + wave * kMfV;  // the wave's first velocity (uniform)
 
   // LDS-DMA of image `img`'s FK grid into buffer `buf` (256-byte pieces dealt over the waves; lanes past
   // the grid re-read its last dword, landing in the buffer's pad)
   const int n_piece = (2 * nfk + 63) >> 6;
   auto stage = [&](int img, int buf) {
     const float* src = reinterpret_cast<const float*>(FK + (int64_t)img * nfk);
+    const int lane = lane_now();
     for (int p = wave; p < n_piece; p += kMfWaves) {
       const int e = min(p * 64 + lane, 2 * nfk - 1);
       __builtin_amdgcn_global_load_lds((gbl_void*)(src + e), (lds_void*)(fks + buf * nbuf + p * 32), 4, 0, 0);
@@ -837,7 +848,6 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
   };
   for (int e = tid; e < L * L; e += kMfWaves * 64) sgs[e] = sg[e];
   for (int e = tid; e < 64; e += kMfWaves * 64) bpad[e] = (e >= 16 && e < 16 + L) ? sg[e - 16] : 0.0;
-  const int boff = 16 + kk - li;  // interior band B[k][j] of K-step s = bpad[boff + 4 s] = sg[4 s + k - j]
   const int t_reg = (nF - kMfV + kMfV - 1) / kMfV;  // regular tiles: rows [16 t, min(16 t + 16, nF - 16))
 
   for (int it = 0; it < n_img; it += GI) {
@@ -851,14 +861,16 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
     // the lane indices and sizes are laundered per pass: the first and last tiles' samples, band values
     // and store addresses do not depend on the images, and hoisting them out of the image loop would hold
     // ~200 registers; recomputing them is a few VALU per tile
-    int li_, kk_, nF_, nV_, va_, vc_, fl_;
+    int li_, kk_, nF_, nV_, va_, vc_, fl_, boff;
     bool vok_;
     auto launder = [&]() {  // also before the last tile: no common subexpression with tile 0 lives across the loop
-      li_ = li;
-      kk_ = kk;
+      const int ln = lane_now();
+      li_ = ln & 15;
+      kk_ = ln >> 4;
       nF_ = nF;
       nV_ = nV;
       asm volatile("" : "+v"(li_), "+v"(kk_), "+s"(nF_), "+s"(nV_));
+      boff = 16 + kk_ - li_;  // interior band B[k][j] of K-step s = bpad[boff + 4 s] = sg[4 s + k - j]
       va_ = vw + li_;
       vok_ = va_ < nV_;
       vc_ = min(va_, nV_ - 1);
@@ -922,6 +934,10 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
       sample(4 * s - 12 + kk_, x[s]);  // this group's samples (an opaque dependency the compiler keeps)
       if (s % 4 == 1) asm volatile("" : "+v"(kk_) : "v"(x[s - 3][0]), "v"(x[s - 2][0]), "v"(x[s - 1][0]), "v"(x[s][0]));
     }
+#pragma unroll
+    for (int s = 10; s < 14; ++s)  // every image's tile-1 samples finished here, not deferred past tile 0
+#pragma unroll
+      for (int g = 0; g < GI; ++g) asm volatile("" : "+v"(x[s][g]));
     Pend pd[4];  // table loads of steps 14 .. 17 (tile 2's new ones), in flight during tiles 0 and 1
 #pragma unroll
     for (int i = 0; i < 4; ++i) pd[i] = tload(4 * (14 + i) - 12 + kk_);
@@ -938,6 +954,8 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
       store(acc, 0, min(kMfV, fl_));
       __builtin_amdgcn_sched_barrier(0);
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(pd[i].base));  // corner reads not hoisted above tile 0
     // regular tiles t = 1 .. t_reg - 1, four per iteration so that the ring slots are static.  Tile t
     // consumes steps 4 t .. 4 t + 9; during it, steps 4 t + 10 .. 4 t + 13 are finished from pd (loaded
     // during tile t - 1) and steps 4 t + 14 .. 4 t + 17 are loaded into pd.
@@ -946,6 +964,16 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
       for (int u = 0; u < 4; ++u) {
         const int t = t0 + u;
         if (t >= t_reg) break;
+#if DVH_FV_MF_LATE
+        // steps 4 t + 10 + i -> slot (4 (u + 1) + 10 + i) & 15  (t = t0 + u, t0 = 1 mod 4), then the next
+        // tile's table loads into the same registers (in flight during this tile's MFMAs)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          tfinish(pd[i], x[(4 * (u + 1) + 10 + i) & 15]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pd[i] = tload(16 * t + 44 + 4 * i + kk_);
+#else
         Pend nx[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) nx[i] = tload(16 * t + 44 + 4 * i + kk_);
@@ -954,6 +982,7 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
         for (int i = 0; i < 4; ++i) {
           tfinish(pd[i], x[(4 * (u + 1) + 10 + i) & 15]);
         }
+#endif
         doublex4 acc[GI];
 #pragma unroll
         for (int g = 0; g < GI; ++g) acc[g] = doublex4{0.0, 0.0, 0.0, 0.0};
@@ -966,8 +995,10 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
           }
         }
         store(acc, kMfV * t, fl_);
+#if !DVH_FV_MF_LATE
 #pragma unroll
         for (int i = 0; i < 4; ++i) pd[i] = nx[i];
+#endif
         // one tile per scheduling region, its samples finished in it
         asm volatile("" ::"v"(x[(4 * (u + 1) + 10) & 15][0]), "v"(x[(4 * (u + 1) + 11) & 15][0]),
                      "v"(x[(4 * (u + 1) + 12) & 15][0]), "v"(x[(4 * (u + 1) + 13) & 15][0]));

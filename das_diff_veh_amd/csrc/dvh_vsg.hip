@@ -123,7 +123,10 @@ __device__ __forceinline__ int pull_unit(uint32_t* counter, int lane) {
 }
 
 #ifndef DVH_PULL_TASKS
-#define DVH_PULL_TASKS 0  // validated launch: correlation waves pull row tasks from a counter (A/B; static stride else)
+// validated launch: correlation waves pull row tasks from a counter instead of a static stride.  -1 (default):
+// the padded engines pull (w = 499: fused launch 4.80 -> 3.99 ms, their task costs vary with the pivot-slice
+// table's coverage), the exact ones keep the stride (synth10k / weights measured no better); 0 / 1: none / all
+#define DVH_PULL_TASKS -1
 #endif
 
 // XCD-aware block order (blocks are dealt round robin over the 8 XCDs, each with its own L2):
@@ -1033,12 +1036,13 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
   if constexpr (Fused<E>::v) {
     if (skip) eng.vflag = vflag;
   }
+  constexpr bool kPull = DVH_PULL_TASKS < 0 ? !EXACT : DVH_PULL_TASKS != 0;
   if (wave < kFft) {
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
 #endif
     stack_tasks<E, EXACT>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
-                          (int64_t)gridDim.x * kFft, DVH_PULL_TASKS ? counter + 1 : nullptr);
+                          (int64_t)gridDim.x * kFft, kPull ? counter + 1 : nullptr);
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif

@@ -32,10 +32,13 @@ def _stager(device, dtype, nbytes):
     return st
 
 
+import ctypes  # noqa: E402
 import os  # noqa: E402
 
 _NTHREADS = max(1, min(16, os.cpu_count() or 1))
-STAGE_MODE = os.environ.get("DVH_STAGE_MODE", "pool")  # pool | torch (A/B of the host copy into pinned memory)
+# the host copy into pinned memory: native (dvh_host_gather on the thread pool, float32 C-contiguous windows;
+# others take the pool path) | pool (np.copyto per window on the thread pool) | torch (torch.stack)
+STAGE_MODE = os.environ.get("DVH_STAGE_MODE", "native")
 
 
 def _pool():
@@ -74,10 +77,20 @@ def stage_windows(hosts, device, out=None, wait=True):
             view = st["pinned"][b].numpy()[:kk * per].view(src).reshape((kk,) + tuple(shape))
             nt = min(kk, _NTHREADS)
             bounds = [kk * q // nt for q in range(nt + 1)]
+            chunk = hosts[a:a + kk]
+            if STAGE_MODE == "native" and all(h.dtype == src and h.flags.c_contiguous for h in chunk):
+                from . import _lib
+                srcs = (ctypes.c_void_p * kk)(*[h.ctypes.data for h in chunk])
+                base = view.ctypes.data
 
-            def run(q):
-                for j in range(bounds[q], bounds[q + 1]):
-                    np.copyto(view[j], hosts[a + j], casting="unsafe")
+                def run(q):  # one native call per thread: no interpreter work per window, the lock released
+                    j0, j1 = bounds[q], bounds[q + 1]
+                    _lib.call("dvh_host_gather", ctypes.c_void_p(base + j0 * per),
+                              ctypes.byref(srcs, j0 * ctypes.sizeof(ctypes.c_void_p)), per, j1 - j0)
+            else:
+                def run(q):
+                    for j in range(bounds[q], bounds[q + 1]):
+                        np.copyto(view[j], chunk[j], casting="unsafe")
             list(pool.map(run, range(nt)))
         with torch.cuda.stream(st["stream"]):
             pin = st["pinned"][b][:kk * per].view(tdt).view((kk,) + tuple(shape))

@@ -33,6 +33,11 @@ const char* dvh_last_error(void);
  * out: int64 [times][k] (host memory). */
 int dvh_random_sample(uint32_t* state, int64_t lo, int64_t n, int32_t k, int32_t times, int64_t* out);
 
+/* Host function: n blocks of nbytes, src[i] -> dst + i * nbytes (host memory, non-temporal stores): the packing
+ * of the drop-in classes' NumPy windows (VirtualShotGathersFromWindows, apis/imaging_classes.py:91-126) into a
+ * pinned staging buffer before their H2D copy.  Thread-safe; callers split the windows over threads. */
+int dvh_host_gather(void* dst, const void* const* src, int64_t nbytes, int32_t n);
+
 /* ---------------------------------------------------------------- virtual shot gathers
  * pass_tab [n_pass][2] = {row0 (= start_idx), pivot_idx};  gather row i is channel row0 + i.
  * seg_tab  [n_pass][R][2 sides][2] = {slice start, slice length} of the row's time slice on the

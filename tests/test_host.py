@@ -435,3 +435,19 @@ def test_native_draws_equal_python_random_sample():
     assert np.array_equal(got, ref)
     with pytest.raises(ValueError):
         bt.draw(5, 5, 1)
+
+
+def test_host_gather_packs_windows():
+    """dvh_host_gather (device.py's staging copy, host only): n windows packed back to back, any alignment."""
+    from das_diff_veh_amd import _lib
+    rng = np.random.default_rng(3)
+    hs = [rng.standard_normal((7, 131)).astype(np.float32) for _ in range(9)]
+    per = hs[0].nbytes
+    srcs = (ctypes.c_void_p * len(hs))(*[h.ctypes.data for h in hs])
+    for off in (0, 4, 12):
+        dst = np.zeros(len(hs) * per + 16, np.uint8)
+        _lib.call("dvh_host_gather", ctypes.c_void_p(dst.ctypes.data + off), ctypes.byref(srcs, 8), per, len(hs) - 1)
+        got = dst[off:off + (len(hs) - 1) * per].view(np.float32).reshape(len(hs) - 1, 7, 131)
+        assert all(np.array_equal(got[j], hs[j + 1]) for j in range(len(hs) - 1))
+        assert not dst[off + (len(hs) - 1) * per:].any() and not dst[:off].any()
+    assert _lib.load().dvh_host_gather(None, None, per, 1) != 0
