@@ -767,6 +767,9 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 #define DVH_FV_MF_LATE 0  // 1: a tile's table loads issued after the previous ones are consumed (half the
                           // in-flight registers, a shorter load-to-use distance)
 #endif
+#ifndef DVH_FV_NT_STORE
+#define DVH_FV_NT_STORE 0  // 1: the f-v tiles stored non-temporally (A/B of the write traffic)
+#endif
 #ifndef DVH_FV_MF_WPE
 #define DVH_FV_MF_WPE (DVH_FV_MF_GI == 1 ? 3 : 2)  // waves per SIMD the kernel is register-budgeted for
 #endif
@@ -920,7 +923,13 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int v = vw + kk_ + 4 * r;
-          if (v < nV_) out_b[(int64_t)v * nF_ + f] = (float)acc[g][r];
+          if (v < nV_) {
+#if DVH_FV_NT_STORE
+            __builtin_nontemporal_store((float)acc[g][r], out_b + (int64_t)v * nF_ + f);
+#else
+            out_b[(int64_t)v * nF_ + f] = (float)acc[g][r];
+#endif
+          }
         }
       }
     };

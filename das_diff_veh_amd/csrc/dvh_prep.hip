@@ -16,7 +16,6 @@
 #include <stdint.h>
 
 #include <algorithm>
-#include <utility>
 
 #include "dvh_common.h"
 #include "dvh.h"
@@ -70,27 +69,6 @@ struct SosCoef {
       v = o;
     }
     return v;
-  }
-  // One skewed step of the cascade: section s (LO <= s <= HI) processes the sample s steps behind section 0, so
-  // the NS sections' updates of a step are independent (NS chains in flight instead of one NS-deep chain per
-  // sample).  pipe[s] holds section s's output of the previous step; section 0 takes u.  Same arithmetic per
-  // sample and section as step().
-  template <int LO, int HI>
-  __device__ __forceinline__ void skew(double (&z0)[NS], double (&z1)[NS], double (&pipe)[NS], double u) const {
-    double nv[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (s >= LO && s <= HI) {
-        const double v = s == 0 ? u : pipe[s > 0 ? s - 1 : 0];
-        const double o = b0[s] * v + z0[s];
-        z0[s] = b1[s] * v - a1[s] * o + z1[s];
-        z1[s] = b2[s] * v - a2[s] * o;
-        nv[s] = o;
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      if (s >= LO && s <= HI) pipe[s] = nv[s];
   }
 };
 
@@ -164,22 +142,8 @@ __global__ __launch_bounds__(64) void sos_transition_kernel(const double* __rest
 // through an LDS tile: cooperative loads (16 lanes per run: each instruction reads 4 contiguous runs of 16
 // samples), the recursion on the lane's own tile row, and (phase C) the outputs written back into the same
 // tile slots and stored cooperatively, again 16 contiguous samples per 16 lanes.
-constexpr int kSosCh = 16;               // samples per chunk (L is a multiple of 32)
-constexpr int kSosLd = 2 * kSosCh + 1;   // tile row: a ring of two chunks, odd stride: conflict-free own-row reads
-
-// steps 0 .. NS - 2 of the skewed cascade: step t runs sections 0 .. t (no output yet)
-template <int NS, int... I>
-__device__ __forceinline__ void sos_prologue(const SosCoef<NS>& c, double (&z0)[NS], double (&z1)[NS], double (&pipe)[NS],
-                                             const double* trow, std::integer_sequence<int, I...>) {
-  (c.template skew<0, I>(z0, z1, pipe, trow[I]), ...);
-}
-// steps L .. L + NS - 2: step L + d runs sections d + 1 .. NS - 1 and outputs sample L - NS + 1 + d
-template <int NS, bool OUT, int... D>
-__device__ __forceinline__ void sos_drain(const SosCoef<NS>& c, double (&z0)[NS], double (&z1)[NS], double (&pipe)[NS],
-                                          double* trow, int L, std::integer_sequence<int, D...>) {
-  ((c.template skew<D + 1, NS - 1>(z0, z1, pipe, 0.0),
-    OUT ? (void)(trow[(L + D - NS + 1) & (2 * kSosCh - 1)] = pipe[NS - 1]) : (void)0), ...);
-}
+constexpr int kSosCh = 16;           // samples per chunk (L is a multiple of 32)
+constexpr int kSosLd = kSosCh + 1;   // tile row stride in doubles: conflict-free own-row reads
 template <typename T, int NS, bool BWD, bool OUT>
 __global__ __launch_bounds__(64) void sos_block_kernel(T* __restrict__ x, double* __restrict__ y, SosGeom G,
                                                         const double* __restrict__ sos, const double* __restrict__ zi,
@@ -262,72 +226,47 @@ __global__ __launch_bounds__(64) void sos_block_kernel(T* __restrict__ x, double
       }
     }
   };
-  // cooperative store of chunk cs's outputs (tile half cs & 1)
-  auto coop_store = [&](int64_t cs) {
-    const int64_t cbase = cs * kSosCh;
-    const int h = (int)(cs & 1) * kSosCh;
-    int64_t rs = r_l;
-    int ks = k_l;
-#pragma unroll 4
-    for (int m = 0; m < 16; ++m) {
-      const int sidx = 4 * m + l4;
-      if (g0 + sidx < n_lanes) {
-        const int64_t i = (int64_t)ks * G.L + cbase + e;
-        if (i < min((int64_t)(ks + 1) * G.L, G.n_ext)) {
-          const double v = tile[sidx * kSosLd + h + e];
-          if (!BWD) {
-            y[rs * G.n_ext + i] = v;
-          } else {
-            // reversed index i is sample n_ext - 1 - i of the extension; the row keeps [padlen, padlen + n_t)
-            const int64_t j = G.n_ext - 1 - i - G.padlen;
-            if (j >= 0 && j < G.n_t) x[rs * G.row_stride + j] = (T)v;
-          }
-        }
-      }
-      ks += 4;
-      while (ks >= G.nb) {
-        ks -= G.nb;
-        ++rs;
-      }
-    }
-  };
-  // Every lane runs L steps of the skewed cascade (a row's shorter last block runs past its end on the zeros
-  // of its tile slots: those outputs are not stored and its end state is not needed), the tile a ring of two
-  // chunks: sample t's input and output share slot t mod 2 kSosCh, and a chunk is stored once the chunk after
-  // it has produced its last outputs (NS - 1 steps behind the inputs).
-  double* trow = tile + lane * kSosLd;
-  double pipe[NS];
-#pragma unroll
-  for (int q = 0; q < NS; ++q) pipe[q] = 0.0;
-  auto steady = [&](int tau) {
-    c.template skew<0, NS - 1>(z0, z1, pipe, trow[tau & (2 * kSosCh - 1)]);
-    if (OUT) trow[(tau - NS + 1) & (2 * kSosCh - 1)] = pipe[NS - 1];
-  };
   if (n_chunks > 0) coop_load(0);
   for (int64_t ch = 0; ch < n_chunks; ++ch) {
-    const int h = (int)(ch & 1) * kSosCh;
+    const int64_t cbase = ch * kSosCh;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) tile[(4 * m + l4) * kSosLd + h + e] = pv[m];
+    for (int m = 0; m < 16; ++m) tile[(4 * m + l4) * kSosLd + e] = pv[m];
     __syncthreads();
-    if (ch + 1 < n_chunks) coop_load((ch + 1) * kSosCh);  // the next chunk's loads in flight under this one
-    const int tau0 = (int)(ch * kSosCh);
-    if (ch == 0) {  // prologue: section s starts at step s
-      sos_prologue<NS>(c, z0, z1, pipe, trow, std::make_integer_sequence<int, NS - 1>{});
-      for (int t = NS - 1; t < kSosCh; ++t) steady(t);
+    if (ch + 1 < n_chunks) coop_load(cbase + kSosCh);  // the next chunk's loads in flight under this one's recursion
+    const int64_t nn = min((int64_t)kSosCh, i1 - i0 - cbase);
+    if (OUT) {
+      for (int t = 0; t < nn; ++t) tile[lane * kSosLd + t] = c.step(z0, z1, tile[lane * kSosLd + t]);
     } else {
-      for (int t = 0; t < kSosCh; ++t) steady(tau0 + t);
+      for (int t = 0; t < nn; ++t) c.step(z0, z1, tile[lane * kSosLd + t]);
     }
     __syncthreads();
-    if (OUT && ch >= 1) {
-      coop_store(ch - 1);
+    if (OUT) {  // cooperative store of the outputs
+      int64_t rs = r_l;
+      int ks = k_l;
+#pragma unroll 4
+      for (int m = 0; m < 16; ++m) {
+        const int sidx = 4 * m + l4;
+        if (g0 + sidx < n_lanes) {
+          const int64_t i = (int64_t)ks * G.L + cbase + e;
+          if (i < min((int64_t)(ks + 1) * G.L, G.n_ext)) {
+            const double v = tile[sidx * kSosLd + e];
+            if (!BWD) {
+              y[rs * G.n_ext + i] = v;
+            } else {
+              // reversed index i is sample n_ext - 1 - i of the extension; the row keeps [padlen, padlen + n_t)
+              const int64_t j = G.n_ext - 1 - i - G.padlen;
+              if (j >= 0 && j < G.n_t) x[rs * G.row_stride + j] = (T)v;
+            }
+          }
+        }
+        ks += 4;
+        while (ks >= G.nb) {
+          ks -= G.nb;
+          ++rs;
+        }
+      }
       __syncthreads();
     }
-  }
-  // drain: the last NS - 1 samples through the later sections
-  sos_drain<NS, OUT>(c, z0, z1, pipe, trow, (int)(n_chunks * kSosCh), std::make_integer_sequence<int, NS - 1>{});
-  if (OUT && n_chunks > 0) {
-    __syncthreads();
-    coop_store(n_chunks - 1);
   }
   if (!OUT && act) {
 #pragma unroll
