@@ -10,8 +10,12 @@ d = sys.argv[1]
 copies, kernels = [], []
 for f in glob.glob(f"{d}/**/*memory_copy_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "HOST_TO_DEVICE" in r.get("Direction", "") or "H2D" in r.get("Direction", ""):
-            copies.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r.get("Bytes", 0) or 0)))
+        if not copies and not kernels:
+            print("columns:", list(r.keys()))
+        kind = " ".join(str(v) for k, v in r.items() if k in ("Direction", "Operation", "Kind"))
+        size = next((int(float(v)) for k, v in r.items() if ("Size" in k or "Bytes" in k) and v), 0)
+        if "HOST_TO_DEVICE" in kind or "H2D" in kind or "HostToDevice" in kind:
+            copies.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), size))
 for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         kernels.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60]))

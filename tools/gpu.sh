@@ -9,8 +9,8 @@
 #   bash tools/gpu.sh prof TAG [workload]        rocprofv3 --kernel-trace --stats of the bench ->
 #                                                gpurun_out/prof_TAG*/ (copy the stats CSV to profiles/)
 #   bash tools/gpu.sh pmc TAG [workload]         PMC passes -> profiles/TAG_pmc_summary[_workload].json
-#   bash tools/gpu.sh final TAG                  end of round: tests + smoke, PMC (synth10k, sliding, weights,
-#                                                timelapse), then `lines`
+#   bash tools/gpu.sh final TAG                  end of round, first call: tests + smoke, PMC (synth10k, sliding,
+#                                                weights, w = 499, timelapse); the second call is `lines`
 #   bash tools/gpu.sh lines TAG                  every bench line with its CPU baseline (synth10k, weights, sliding,
 #                                                timelapse, w = 499, prep, bootstrap, speeds-host) + kernel stats
 set -o pipefail
@@ -70,11 +70,10 @@ case $mode in
   final)
     tag=$1
     run_tests || exit 1
-    for wl in synth10k sliding weights; do
+    for wl in synth10k sliding weights w499; do
       bash "$0" pmc $tag $wl || exit 1
     done
     bash tools/pmc_timelapse.sh $tag > gpurun_out/pmc_tl.log 2>&1 || { echo pmc tl failed; tail -5 gpurun_out/pmc_tl.log; exit 1; }
-    bash "$0" lines $tag || exit 1
     rm -rf gpurun_out/pmc_${tag}* ;;
   lines)
     tag=$1
