@@ -104,6 +104,20 @@ def _stage(windows, idx, device):
     return lambda: to_device_f32(arrs, device)
 
 
+def _rows_of(batch_fn, idx, n, memo):
+    """Callable giving rows idx of the staged batch batch_fn() (all n windows; evaluated once, kept in memo):
+    the batch itself when idx is all of them in order."""
+    def rows():
+        import torch
+        if "batch" not in memo:
+            memo["batch"] = batch_fn()
+        full = memo["batch"]
+        if len(idx) == n and all(i == k for k, i in enumerate(idx)):
+            return full
+        return full[torch.as_tensor(np.asarray(idx, dtype=np.int64), device=full.device)]
+    return rows
+
+
 def gathers(windows, prm: VsgParams, device=None):
     """Per-pass gathers as float64 NumPy arrays, plus each pass's gather axes."""
     device = device or default_device()
@@ -124,11 +138,19 @@ def stacked(windows, prm: VsgParams, slots=None, n_slot=1, device=None, chunk=8,
     device = device or default_device()
     slots = np.zeros(len(windows), dtype=np.int64) if slots is None else np.asarray(slots)
     counts = np.bincount(slots, minlength=n_slot) if counts is None else np.asarray(counts)
+    # windows of one data shape (the notebooks' case) start their copies before anything else, in the caller's
+    # order; a group takes its rows of the staged batch
+    early = None
+    if windows and len({np.shape(w.data) for w in windows}) == 1:
+        early = _stage(windows, range(len(windows)), device)
     groups, axes = _groups(windows, prm)
     if len({key[1:3] for key in groups}) != 1:
         raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
-    # every group's window copies start first (background thread), the tables are formed meanwhile
-    staged = [(idx, key, _stage(windows, idx, device)) for key, idx in groups.items()]
+    if early is not None:
+        memo = {}
+        staged = [(idx, key, _rows_of(early, idx, len(windows), memo)) for key, idx in groups.items()]
+    else:  # every group's window copies start first (background thread), the tables are formed meanwhile
+        staged = [(idx, key, _stage(windows, idx, device)) for key, idx in groups.items()]
     out = None
     for idx, key, data_fn in staged:
         plan = _plan(windows, idx, key, prm, device)
