@@ -145,5 +145,24 @@ def to_device_f32(arrays, device=None):
     return torch.from_numpy(host).to(device, non_blocking=False)
 
 
+def upload(arrays, device):
+    """Small host arrays -> device tensors through ONE pinned buffer and ONE asynchronous copy on the current
+    stream (the caller does not wait; kernels queued after it on the stream see the data).  A plan's few
+    tables cost one DMA queue slot instead of one blocking copy each, which matters while the window staging
+    keeps the H2D engine busy with 128 MB chunks."""
+    arrs = [np.ascontiguousarray(a) for a in arrays]
+    offs, total = [], 0
+    for a in arrs:
+        offs.append(total)
+        total += (a.nbytes + 15) & ~15
+    host = torch.empty(max(total, 16), dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    for a, o in zip(arrs, offs):
+        hv[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+    dev = host.to(device, non_blocking=True)  # the pinned block is held by torch's host allocator until the copy ends
+    return [dev[o:o + a.nbytes].view(torch.from_numpy(np.empty(0, a.dtype)).dtype).view(a.shape)
+            for a, o in zip(arrs, offs)]
+
+
 def to_host_f64(t):
     return t.detach().to("cpu").numpy().astype(np.float64)

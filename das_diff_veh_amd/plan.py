@@ -298,10 +298,9 @@ class DevicePlan:
         if int(en.max()) > self.n_ch:
             raise ValueError("gather rows beyond the window")
         dev = trk_x.device
-        self.pass_tab = torch.from_numpy(np.stack([st, pv], 1).astype(np.int32)).to(dev)
-        self.pivot_x = torch.from_numpy(np.ascontiguousarray(piv)).to(dev)
-        self._x = torch.from_numpy(np.ascontiguousarray(x)).to(dev)
-        self._t = torch.from_numpy(np.ascontiguousarray(t)).to(dev)
+        from .device import upload
+        self.pass_tab, self.pivot_x, self._x, self._t = upload(
+            [np.stack([st, pv], 1).astype(np.int32), piv, x, t], dev)
         self.trk_x, self.trk_t = trk_x, trk_t
         self.trk_len = trk_len.to(device=dev, dtype=torch.int32)
         if seg_out is not None:  # caller-owned table buffer (e.g. shared by a pipeline's batches)
@@ -388,7 +387,8 @@ def pack_trajectories(trajectories, device):
             o = np.argsort(vx, axis=1, kind="stable")
             vx, vt = np.take_along_axis(vx, o, 1), np.take_along_axis(vt, o, 1)
         tx[idx, :k], tt[idx, :k] = vx, vt
-    return (torch.from_numpy(tx).to(device), torch.from_numpy(tt).to(device), torch.from_numpy(ln).to(device))
+    from .device import upload
+    return tuple(upload([tx, tt, ln], device))
 
 
 # ------------------------------------------------------------------------------------------------
