@@ -39,7 +39,7 @@ _NTHREADS = max(1, min(16, os.cpu_count() or 1))
 # the host copy into pinned memory: native (dvh_host_gather on the thread pool, float32 C-contiguous windows;
 # others take the pool path) | pool (np.copyto per window on the thread pool) | torch (torch.stack)
 STAGE_MODE = os.environ.get("DVH_STAGE_MODE", "native")
-STAGE_RAMP = os.environ.get("DVH_STAGE_RAMP", "0") == "1"  # measured no better (28.0 / 29.1 vs 32.5 / 29.8 k windows/s)
+STAGE_RAMP = int(os.environ.get("DVH_STAGE_RAMP", "0"))  # 0: off, r: first chunk k / r windows, doubling up to k
 
 
 def _pool():
@@ -67,9 +67,9 @@ def stage_windows(hosts, device, out=None, wait=True):
     st = _stager(device, src, k * per)
     pool = _pool()
     tdt = torch.float32 if src == np.float32 else torch.float64
-    # chunk starts: with STAGE_RAMP the first chunks are k / 8, k / 4, k / 2 windows, so that the first H2D copy
-    # starts after a short host copy instead of a full one
-    starts, a, kc = [], 0, max(1, k // 8) if STAGE_RAMP else k
+    # chunk starts: with STAGE_RAMP = r the first chunks are k / r, 2 k / r, ... windows, so that the first H2D
+    # copy starts after a short host copy instead of a full one
+    starts, a, kc = [], 0, max(1, k // STAGE_RAMP) if STAGE_RAMP > 0 else k
     while a < n:
         starts.append((a, min(kc, n - a)))
         a += kc

@@ -16,7 +16,7 @@ import sys
 import numpy as np
 
 from .device import default_device, to_device_f32, to_host_f64
-from .plan import DevicePlan, VsgParams, pack_trajectories, spatial_indices, window_lengths
+from .plan import DevicePlan, VsgParams, pack_trajectories_checked, spatial_indices, window_lengths
 from .vsg import StackSchedule, vsg_gathers, vsg_stack, vsg_stack_validated
 
 
@@ -42,7 +42,7 @@ def _axes(win, prm: VsgParams):
 def _shared_or_stacked(arrays):
     """One 1-D axis when every window has the same one, else the [n, L] stack of them."""
     a0 = np.asarray(arrays[0], dtype=np.float64)
-    if all(np.array_equal(a0, a) for a in arrays[1:]):
+    if all(a is arrays[0] or np.array_equal(a0, a) for a in arrays[1:]):  # windows often share the axis object
         return a0
     return np.stack([np.asarray(a, dtype=np.float64) for a in arrays])
 
@@ -51,10 +51,15 @@ def _axes_all(windows, prm: VsgParams):
     """_axes of every window, evaluated once per distinct (channel axis, dt): notebook windows of one fiber
     section share their axes' values (the reference's per-window argmax searches give the same answer)."""
     memo, keys, axes = {}, [], []
+    last = (None, None, None)  # (x_axis object, t_axis object, memo key): windows sharing the axis objects
     for w in windows:
-        x = np.asarray(w.x_axis, dtype=np.float64)
-        t = np.asarray(w.t_axis, dtype=np.float64)
-        mk = (x.tobytes(), t[:2].tobytes()) if t.size >= 2 else None
+        if w.x_axis is last[0] and w.t_axis is last[1] and last[2] is not None:
+            mk = last[2]
+        else:
+            x = np.asarray(w.x_axis, dtype=np.float64)
+            t = np.asarray(w.t_axis, dtype=np.float64)
+            mk = (x.tobytes(), t[:2].tobytes()) if t.size >= 2 else None
+            last = (w.x_axis, w.t_axis, mk)
         if mk is None or mk not in memo:
             r = _axes(w, prm)
             if mk is None:
@@ -64,8 +69,41 @@ def _axes_all(windows, prm: VsgParams):
             memo[mk] = r
         k, a = memo[mk]
         keys.append(k)
-        axes.append(GatherAxes(a.gather_x_axis.copy(), a.gather_t_axis.copy()))  # each image owns its axes
-    return keys, axes
+        axes.append(a)
+    return keys, _OwnAxes(axes)
+
+
+class _OwnAxes(list):
+    """Every pass's GatherAxes; passes of one (channel axis, dt) share one memo entry, which an entry's first
+    access replaces by the pass's own copy, so that every image still owns its axes (as the reference's
+    per-window objects do) while the callers that read only a few entries (get_images reads the first) do not
+    pay a copy per window."""
+
+    def __init__(self, items):
+        super().__init__(items)
+        self._own = bytearray(len(self))
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        i = range(len(self))[i]
+        a = super().__getitem__(i)
+        if not self._own[i]:
+            a = GatherAxes(a.gather_x_axis.copy(), a.gather_t_axis.copy())
+            super().__setitem__(i, a)
+            self._own[i] = 1
+        return a
+
+    def __setitem__(self, i, v):
+        super().__setitem__(i, v)
+        if isinstance(i, slice):
+            for j in range(*i.indices(len(self))):
+                self._own[j] = 1
+        else:
+            self._own[range(len(self))[i]] = 1
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
 
 
 def _groups(windows, prm: VsgParams):
@@ -74,15 +112,15 @@ def _groups(windows, prm: VsgParams):
     groups = {}
     for i, (w, k) in enumerate(zip(windows, keys)):
         groups.setdefault((tuple(w.data.shape),) + k, []).append(i)
-    return groups, list(axes)
+    return groups, axes
 
 
 def _plan(windows, idx, key, prm: VsgParams, device):
     ws = [windows[i] for i in idx]
-    trk = pack_trajectories([(w.veh_state_x, w.veh_state_t) for w in ws], device)
+    trk, bad = pack_trajectories_checked([(w.veh_state_x, w.veh_state_t) for w in ws], device)
     plan = DevicePlan(_shared_or_stacked([w.x_axis for w in ws]), _shared_or_stacked([w.t_axis for w in ws]),
                       *trk, prm, key[0][0])
-    return plan.check()
+    return plan.check(bad)  # no device round trip (the H2D engine may be busy with the windows' staging)
 
 
 def group_windows(windows, prm: VsgParams, device):

@@ -348,9 +348,11 @@ class DevicePlan:
         sub.geoms = None
         return sub
 
-    def check(self):
-        """Raise like interp1d would for passes whose trajectory could not be evaluated (synchronises)."""
-        bad = np.nonzero(self.status.cpu().numpy())[0]
+    def check(self, host_status=None):
+        """Raise like interp1d would for passes whose trajectory could not be evaluated: from host_status
+        (pack_trajectories_checked's, the same rule) when given, else from the kernel's (synchronises)."""
+        st = self.status.cpu().numpy() if host_status is None else np.asarray(host_status)
+        bad = np.nonzero(st)[0]
         if bad.size:
             raise ValueError(f"passes {bad.tolist()[:8]}: trajectory needs >= 2 strictly ascending tracked points")
         return self
@@ -370,25 +372,41 @@ def pack_trajectories(trajectories, device):
     """[(veh_state_x, veh_state_t), ...] -> padded float64 device tensors (trk_x, trk_t [n, L]) and
     trk_len [n] int32, the layout dvh_pass_geometry reads.  Each trajectory is ordered by x with a
     stable sort first, as interp1d does (its mergesort of the abscissae)."""
-    import torch
+    return pack_trajectories_checked(trajectories, device)[0]
+
+
+def pack_trajectories_checked(trajectories, device):
+    """pack_trajectories, plus each pass's status as dvh_pass_geometry forms it (1: fewer than 2 points or not
+    strictly ascending once sorted, NaN included), computed here from the same sorted rows so that
+    DevicePlan.check() needs no device round trip."""
     n = len(trajectories)
     lens = np.array([len(vx) for vx, _ in trajectories], dtype=np.int64)
     L = max(1, int(lens.max()) if n else 1)
-    tx = np.zeros((n, L))
-    tt = np.zeros((n, L))
+    one = n > 0 and int(lens.min()) == L  # every pass the same length: the block is the padded layout itself
+    tx = None if one else np.zeros((n, L))
+    tt = None if one else np.zeros((n, L))
     ln = lens.astype(np.int32)
-    # trajectories of one length are ordered together: a row-wise stable argsort equals each row's mergesort,
-    # and rows already ascending (the tracker's output) are copied as they are
+    bad = (lens < 2).astype(np.int32)
+    # trajectories of one length are ordered together (one [m, k] block per length: the tracker's passes share
+    # a handful of lengths): a row-wise stable argsort equals each row's mergesort, and rows already ascending
+    # (the tracker's output) are copied as they are
     for k in np.unique(lens):
         idx = np.flatnonzero(lens == k)
         vx = np.array([np.asarray(trajectories[i][0], dtype=np.float64) for i in idx]).reshape(idx.size, k)
         vt = np.array([np.asarray(trajectories[i][1], dtype=np.float64) for i in idx]).reshape(idx.size, k)
-        if k > 1 and not np.all(vx[:, 1:] > vx[:, :-1]):
+        asc = vx[:, 1:] > vx[:, :-1]
+        if k > 1 and not np.all(asc):
             o = np.argsort(vx, axis=1, kind="stable")
             vx, vt = np.take_along_axis(vx, o, 1), np.take_along_axis(vt, o, 1)
-        tx[idx, :k], tt[idx, :k] = vx, vt
+            asc = vx[:, 1:] > vx[:, :-1]
+        if k > 1:
+            bad[idx] |= ~np.all(asc, axis=1)  # a pair not strictly ascending (NaN included)
+        if one:
+            tx, tt = vx, vt
+        else:
+            tx[idx, :k], tt[idx, :k] = vx, vt
     from .device import upload
-    return tuple(upload([tx, tt, ln], device))
+    return tuple(upload([tx, tt, ln], device)), bad
 
 
 # ------------------------------------------------------------------------------------------------

@@ -106,6 +106,30 @@ def test_bad_trajectory_status(device):
         dev.check()
 
 
+def test_host_trajectory_status_equals_kernel(device):
+    """pack_trajectories_checked's host status (engine.stacked's check without a device round trip) equals the
+    geometry kernel's on sorted, reversed, repeated, NaN, single-point and empty trajectories."""
+    import torch
+
+    from das_diff_veh_amd.plan import DevicePlan, VsgParams, pack_trajectories_checked
+    g = gio.load("vsg_w500")
+    w = gio.oracle_window(g, 0)
+    vx, vt = w["veh_state_x"], w["veh_state_t"]
+    nan_x = vx.copy()
+    nan_x[7] = np.nan
+    shuffled = np.random.default_rng(1).permutation(vx.size)
+    trks = [(vx, vt), (vx[::-1], vt[::-1]), (np.r_[vx[:5], vx[4:]], np.r_[vt[:5], vt[4:]]), (vx[:1], vt[:1]),
+            (nan_x, vt), (vx[shuffled], vt[shuffled]), (vx[:0], vt[:0]), (vx[:2], vt[:2]), (vx[[1, 1]], vt[:2])]
+    (tx, tt, tl), bad = pack_trajectories_checked(trks, device)
+    dev = DevicePlan(w["x_axis"], w["t_axis"], tx, tt, tl, VsgParams(pivot=700, start_x=500, end_x=900),
+                     w["data"].shape[0])
+    torch.cuda.synchronize()
+    assert bad.tolist() == dev.status.cpu().numpy().tolist() == [0, 0, 1, 1, 1, 0, 1, 0, 1]
+    with pytest.raises(ValueError):
+        dev.check(bad)
+    assert dev.check(np.zeros(len(trks), np.int32)) is dev
+
+
 @pytest.mark.parametrize("seed,npts", [(3, 400), (4, 1500)])  # 1500: beyond the kernel's LDS-staged trajectories
 def test_irregular_axes_geometry(device, seed, npts):
     """Non-uniform t axes (jittered steps, a 20x-denser stretch, repeated samples) and trajectories

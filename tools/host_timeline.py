@@ -44,7 +44,7 @@ wrap(engine, "_plan", "plan")
 wrap(engine, "vsg_stack_validated", "launch")
 wrap(engine, "vsg_stack", "launch")
 wrap(VirtualShotGathersFromWindows, "get_images", "get_images")
-wrap(engine, "pack_trajectories", "  pack")
+wrap(engine, "pack_trajectories_checked", "  pack")
 wrap(engine, "_shared_or_stacked", "  axes")
 wrap(engine.DevicePlan, "__init__", "  plan_init")
 wrap(engine.DevicePlan, "derive", "  derive")
