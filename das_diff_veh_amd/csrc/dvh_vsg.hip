@@ -794,6 +794,9 @@ constexpr int kScanDepth = DVH_SCAN_DEPTH;  // 16-byte loads per lane in flight
 #ifndef DVH_SCAN_AUX
 #define DVH_SCAN_AUX 2
 #endif
+#ifndef DVH_SCAN_SLEEP
+#define DVH_SCAN_SLEEP 0
+#endif
 constexpr int kScanAux = DVH_SCAN_AUX;  // cache policy of the scan's buffer loads (nt; allocating loads measured 4 %
                                         // slower on synth10k)
 
@@ -826,6 +829,9 @@ __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int n
     off += 1024;
   }
   for (int s0 = 0; s0 < nsteps; s0 += kScanDepth) {
+#if DVH_SCAN_SLEEP
+    __builtin_amdgcn_s_sleep(DVH_SCAN_SLEEP);  // A/B: a throttled stream (64 x N clocks per 16 KB of a wave)
+#endif
 #pragma unroll
     for (int d = 0; d < kScanDepth; ++d) {
       const u32x4 v = r[d] & 0x7fffffffu;
