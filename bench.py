@@ -131,7 +131,8 @@ def launch_ranks(argv, n, poll_s=0.2, grace_s=10.0):
                 p.kill()
                 p.wait()
     out0.seek(0)
-    sys.stdout.write(out0.read())
+    for line in out0.read().splitlines(True):  # the JSON line on stdout, anything else rank 0 printed on stderr
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
     sys.stdout.flush()
     rcs = [p.returncode for p in procs]
     rc = 0
@@ -1206,7 +1207,18 @@ def main():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         # RCCL over xGMI, one rank per GPU; DVH_DIST_BACKEND=gloo rehearses the multi-rank step with
         # several ranks on one GPU (RCCL refuses that), reducing through host copies
-        dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
+        # the collective libraries' own connection messages (Gloo prints one per rank on stdout) go to stderr:
+        # stdout carries only rank 0's JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend, device_id=device if backend == "nccl" else None)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"[bench] world size {dist.get_world_size()} != --gpus {args.gpus}")
 
