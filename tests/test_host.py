@@ -451,3 +451,27 @@ def test_host_gather_packs_windows():
         assert all(np.array_equal(got[j], hs[j + 1]) for j in range(len(hs) - 1))
         assert not dst[off + (len(hs) - 1) * per:].any() and not dst[:off].any()
     assert _lib.load().dvh_host_gather(None, None, per, 1) != 0
+
+
+def test_rows_of_staged_batch():
+    """engine._rows_of: a group's rows of the early-staged batch (evaluated once), the batch itself when the group
+    is every window in order; engine._OwnAxes: each pass owns its axes, copied on first access."""
+    import torch
+
+    from das_diff_veh_amd import engine
+    calls = []
+
+    def batch():
+        calls.append(1)
+        return torch.arange(12.0).view(6, 2)
+    memo = {}
+    whole = engine._rows_of(batch, range(6), 6, memo)()
+    part = engine._rows_of(batch, [1, 3, 5], 6, memo)()
+    assert len(calls) == 1 and whole.shape == (6, 2)
+    assert torch.equal(part, whole[[1, 3, 5]])
+    ax = engine.GatherAxes(np.arange(3.0), np.arange(2.0))
+    own = engine._OwnAxes([ax, ax, ax])
+    a1 = own[1]
+    a1.gather_x_axis[0] = 7.0
+    assert own[1] is a1 and own[0].gather_x_axis[0] == 0.0 and ax.gather_x_axis[0] == 0.0
+    assert len(list(own)) == 3 and own[-1] is own[2] and [a is b for a, b in zip(own[0:2], own[0:2])] == [True, True]
