@@ -708,30 +708,23 @@ __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2*
   for (int p = blockIdx.x * 4 + wave; p < A.n_pass; p += gridDim.x * 4) {
     const int row0 = sld(A.pass_tab + 2 * p), pivot = sld(A.pass_tab + 2 * p + 1);
     const RowTask tp = make_task(A, p, pivot - row0), tl = make_task(A, p, A.R - 1), t0 = make_task(A, p, 0);
-    int st[kTabEnt], nw[kTabEnt];
-    st[0] = tp.a_f;
-    nw[0] = tp.nwin_f;
-    st[1] = tp.a_o;
-    nw[1] = tp.nwin_o;
-    st[2] = tl.a_f;
-    nw[2] = tl.ch > pivot ? tl.nwin_f : 0;
-    st[3] = t0.a_o;
-    nw[3] = t0.ch < pivot ? t0.nwin_o : 0;
+    int st0 = tp.a_f, st1 = tp.a_o, st2 = tl.a_f, st3 = t0.a_o;
+    int nw0 = tp.nwin_f, nw1 = tp.nwin_o, nw2 = tl.ch > pivot ? tl.nwin_f : 0, nw3 = t0.ch < pivot ? t0.nwin_o : 0;
     // an entry holds kTabSub sub-windows: a pass with more (time_window_to_xcorr > 2 wlen) is marked unusable
     // (every head nwin = -1, nothing transformed) and its row tasks take the plain z = P + i R path
-    const bool fits = nw[0] <= kTabSub && nw[1] <= kTabSub && nw[2] <= kTabSub && nw[3] <= kTabSub;
-    if (!fits) {
-#pragma unroll
-      for (int e = 0; e < kTabEnt; ++e) nw[e] = -1;
-    }
-    if (lane < 2 * kTabEnt) head[(int64_t)p * 2 * kTabEnt + lane] = (lane & 1) ? nw[lane >> 1] : st[lane >> 1];
+    static_assert(kTabEnt == 4, "entries: pivot forward / other side, far-row forward / other side");
+    if (!(nw0 <= kTabSub && nw1 <= kTabSub && nw2 <= kTabSub && nw3 <= kTabSub)) nw0 = nw1 = nw2 = nw3 = -1;
+    // entry values by selects among scalars (a run-time index into a stack array went to scratch)
+    auto pick = [](int e, int a0, int a1, int a2, int a3) { return e == 0 ? a0 : e == 1 ? a1 : e == 2 ? a2 : a3; };
+    if (lane < 2 * kTabEnt)
+      head[(int64_t)p * 2 * kTabEnt + lane] = (lane & 1) ? pick(lane >> 1, nw0, nw1, nw2, nw3) : pick(lane >> 1, st0, st1, st2, st3);
     // the slices (e, q), q < kTabSub, two per transform; absent ones are zero
 #pragma unroll 1
     for (int s0 = 0; s0 < kTabSub * kTabEnt; s0 += 2) {
       const int e0 = s0 / kTabSub, q0 = s0 % kTabSub, e1 = (s0 + 1) / kTabSub, q1 = (s0 + 1) % kTabSub;
-      const bool h0 = q0 < nw[e0], h1 = q1 < nw[e1];
-      const float* x0 = tp.piv + st[e0] + q0 * A.hop;
-      const float* x1 = tp.piv + st[e1] + q1 * A.hop;
+      const bool h0 = q0 < pick(e0, nw0, nw1, nw2, nw3), h1 = q1 < pick(e1, nw0, nw1, nw2, nw3);
+      const float* x0 = tp.piv + pick(e0, st0, st1, st2, st3) + q0 * A.hop;
+      const float* x1 = tp.piv + pick(e1, st0, st1, st2, st3) + q1 * A.hop;
       uint32_t nz0 = 0, nz1 = 0;
       const float2* X = nullptr;
       if (h0 || h1) {
