@@ -4,9 +4,9 @@
 Default workload = BASELINE.json configs[2], "synth10k", the largest single-GPU configuration:
 10,240 synthetic vehicle passes of 1,024 channels x 8,192 samples (8.16 m, dt = 0.004 s), one pivot
 (channel 512), every channel a gather row (R = 1,023), speed-tercile classes.  The job's 335 GB of
-fp32 windows exceed HBM, so a pool of 512 windows is resident and one step images the 10,240 passes
-as 20 batches over that pool, each batch with its own 512 trajectories (window contents repeat across
-batches, the per-pass work does not).
+fp32 windows exceed HBM, so a pool of 2,048 windows (69 GB) is resident and one step images the 10,240
+passes as 5 batches over that pool, each batch with its own 2,048 trajectories (window contents repeat
+across batches, the per-pass work does not).
 
 One step, per batch, all on the device and on one stream:
   1. the batch's index tables from its trajectories      dvh_pass_geometry   (preprocessing_window)
@@ -67,6 +67,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--chunk", type=int, default=8, help="passes per stack task (one wave, one gather row)")
+    ap.add_argument("--pool", type=int, default=None, help="resident windows (= passes per stack launch) of the pool "
+                    "workloads (default: the workload's)")
     ap.add_argument("--sliding-merge", type=int, default=None,
                     help="sliding: batches of trajectories per stack launch (default: all 49 in one launch)")
     ap.add_argument("--separate-validity", action="store_true",
@@ -194,9 +196,9 @@ VALU_PEAK_INSTR_S = 256 * 4 * 2.4e9 / 2
 
 WORKLOADS = {
     "synth10k": dict(kind="pool", config="configs[2]", pivot=(4178.0, 0.0, 8400.0), n_total=10240, n_ch=1024, n_t=8192,
-                     pool=512, x_first=0.37, gen_chunk=8, track_half=4300,
+                     pool=2048, x_first=0.37, gen_chunk=8, track_half=4300,
                      desc="configs[2]: synthetic 10,240 passes x 1024 ch x 8192, pivot = channel 512, all channels "
-                          "(R = 1023), speed-tercile classes; 20 batches of 512 over a resident window pool, each "
+                          "(R = 1023), speed-tercile classes; 5 batches of 2048 over a resident window pool (69 GB), each "
                           "batch with its own trajectories"),
     "weights": dict(kind="resident", config="configs[1]",
                     pivots=[(700.0, 500.0, 900.0, (103, 1058, 734)), (680.0, 480.0, 880.0, (103, 1058, 734))],
@@ -1190,6 +1192,10 @@ def host_main(args, world, rank, device):
 
 def main():
     args = _ARGS
+    if args.pool:
+        if "pool" not in WORKLOADS[args.workload]:
+            raise SystemExit(f"[bench] --pool: workload {args.workload} has no window pool")
+        WORKLOADS[args.workload]["pool"] = args.pool
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

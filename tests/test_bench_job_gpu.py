@@ -90,10 +90,10 @@ def test_synth10k_job(device):
 
 def test_synth10k_full_job_properties(device):
     """The bench's synth10k job at its FULL size (BASELINE configs[2]: 10 240 passes of 1 024 x 8 192 as
-    20 batches of 512 over the window pool), through size-independent properties:
+    5 batches of 2 048 over the window pool), through size-independent properties:
       * the validated launch (correlation + class stack + validity of every window sample in one launch)
         equals the separate path (dvh_window_sumsq launch, then the plain stack launch) to 1e-5;
-      * stacking is linear: the step's class stacks equal the count-weighted sum of the 20 batches'
+      * stacking is linear: the step's class stacks equal the count-weighted sum of the batches'
         own class means;
       * every class image is finite and a step is reproducible to fp32 atomic-order rounding."""
     import torch
