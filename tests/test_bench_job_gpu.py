@@ -100,7 +100,7 @@ def test_synth10k_full_job_properties(device):
 
     import bench
     job = bench.build("synth10k", device, 1, 0)
-    assert len(job.batches) == 20 and sum(b.plan.n_pass for b in job.batches) == 10240
+    assert len(job.batches) == 5 and sum(b.plan.n_pass for b in job.batches) == 10240
     bench.step(job, 1, fused=True)
     fused, fv = job.stack.clone(), job.fv.clone()
     bench.step(job, 1, fused=False)
