@@ -1,6 +1,8 @@
 """Device selection and host<->device staging for the drop-in API (PyTorch is plumbing only)."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -15,7 +17,7 @@ def default_device():
 # by a thread pool into one of two pinned buffers (in the windows' own dtype, no host-side conversion), sent
 # by an asynchronous H2D copy on a side stream, and converted to float32 on the device, so that the host copy
 # of chunk k + 1 runs while chunk k crosses PCIe.
-STAGE_BYTES = 128 << 20
+STAGE_BYTES = int(os.environ.get("DVH_STAGE_MB", "128")) << 20
 _STAGE = {}
 
 
@@ -33,7 +35,6 @@ def _stager(device, dtype, nbytes):
 
 
 import ctypes  # noqa: E402
-import os  # noqa: E402
 
 _NTHREADS = max(1, min(16, os.cpu_count() or 1))
 # the host copy into pinned memory: native (dvh_host_gather on the thread pool, float32 C-contiguous windows;
