@@ -123,6 +123,26 @@ def test_synth10k_full_job_properties(device):
     assert float((job.stack - fused).abs().max()) <= 1e-5 * scale
 
 
+def test_synth10k_w499_full_job_properties(device):
+    """The bench's synth10k job at w = 499 (`bench.py --w499`: dt = 0.004000000000001336, the zero-padded
+    1 024-point engine) at FULL size: the validated launch equals the separate path (window_sumsq, then the
+    plain padded stack kernel) to 1e-5, every class image is finite and a step is reproducible."""
+    import bench
+    from das_diff_veh_amd.synth import DT_W499
+    wl = dict(bench.WORKLOADS["synth10k"], t0=DT_W499)
+    job = bench.build_pool(wl, device, 1, 0, "weak", chunk=8)
+    assert job.batches[0].plan.w == 499 and sum(b.plan.n_pass for b in job.batches) == 10240
+    bench.step(job, 1, fused=True)
+    fused, fv = job.stack.clone(), job.fv.clone()
+    bench.step(job, 1, fused=False)
+    sep = job.stack.clone()
+    scale = float(sep.abs().max())
+    assert scale > 0 and float((fused - sep).abs().max()) <= 1e-5 * scale
+    assert bool(fv.isfinite().all()) and bool(fused.isfinite().all())
+    bench.step(job, 1, fused=True)
+    assert float((job.stack - fused).abs().max()) <= 1e-5 * scale
+
+
 def test_sliding_job(device):
     """bench.build_sliding as built (configs[3]'s job at a reduced size): per-batch trajectories over a resident
     pool, (class, pivot) slots with the fixed 20 / 25 m/s class edges, batches merged into one UnitPlan.concat
