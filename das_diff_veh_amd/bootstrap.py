@@ -102,6 +102,9 @@ def ridges_launch(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25
     return out, status, picks
 
 
+_DISP_PLANS = {}  # (nch, w, dt, freqs, vels) -> DispPlan, shared by GatherCache instances
+
+
 class GatherCache:
     """Per-pass gathers [n, R, w] of a window list on the device, computed once
     (VirtualShotGathersFromWindows.get_images' per-pass images: norm=False, two-sided)."""
@@ -150,8 +153,16 @@ class GatherCache:
         e = int(np.abs(self.gx - end_x).argmin())
         key = (s, e, id(freqs), id(vels))
         if key not in self._disp:
-            dt = self.gt[1] - self.gt[0]
-            self._disp[key] = (s, e, DispPlan(e + 1 - s, self.plan.w, 8.16, dt, freqs, vels))
+            dt = float(self.gt[1] - self.gt[0])
+            # plans are shared across caches of one geometry (a convergence test per class builds a new cache;
+            # the plan's host tables and their device copies are the same)
+            pkey = (e + 1 - s, self.plan.w, dt, np.asarray(freqs, dtype=np.float64).tobytes(),
+                    np.asarray(vels, dtype=np.float64).tobytes())
+            if pkey not in _DISP_PLANS:
+                if len(_DISP_PLANS) >= 16:
+                    _DISP_PLANS.pop(next(iter(_DISP_PLANS)))
+                _DISP_PLANS[pkey] = DispPlan(e + 1 - s, self.plan.w, 8.16, dt, freqs, vels)
+            self._disp[key] = (s, e, _DISP_PLANS[pkey])
         return self._disp[key]
 
     def resample_stacks(self, sel, start_x=-150, end_x=0, out=None):
@@ -171,6 +182,39 @@ class GatherCache:
         base = self.G[:, s:e + 1, :]
         _lib.call("dvh_select_mean", _lib.ptr(base), R * w, (e + 1 - s) * w, _lib.ptr(sel_t), B, k, _lib.ptr(out),
                   (e + 1 - s) * w, _lib.stream_of(self.device))
+        return out
+
+    def resample_stacks_sizes(self, sels, start_x=-150, end_x=0, out=None):
+        """resample_stacks of several draw sets (sels: list of [B_k, k] arrays, e.g. one per bootstrap size) into
+        consecutive rows of one [sum B_k, nch, w] buffer: every selection crosses to the device in ONE
+        asynchronous copy (device.upload) and each set is one select_mean launch on it, so the host never waits
+        between them."""
+        import ctypes
+
+        from .device import upload
+        sels = [np.asarray(x, dtype=np.int32) for x in sels]
+        if not sels or any(x.ndim != 2 or x.size == 0 for x in sels):
+            raise ValueError("selections must be [B, k] pass indices")
+        flat = np.concatenate([x.reshape(-1) for x in sels])
+        if flat.min() < 0 or flat.max() >= self.n:
+            raise ValueError("selections must be [B, k] pass indices")
+        s, e, _ = self.disp_plan(start_x, end_x)
+        w, R = self.plan.w, self.plan.R
+        B = sum(x.shape[0] for x in sels)
+        rows = (e + 1 - s) * w
+        if out is None:
+            out = torch.empty((B, e + 1 - s, w), dtype=torch.float32, device=self.device)
+        elif tuple(out.shape) != (B, e + 1 - s, w) or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous float32 [{B}, {e + 1 - s}, {w}] tensor")
+        (sel_t,) = upload([flat], self.device)
+        base = self.G[:, s:e + 1, :]
+        off = b0 = 0
+        for x in sels:
+            Bk, k = x.shape
+            _lib.call("dvh_select_mean", _lib.ptr(base), R * w, rows, ctypes.c_void_p(sel_t.data_ptr() + 4 * off), Bk,
+                      k, ctypes.c_void_p(out.data_ptr() + 4 * b0 * rows), rows, _lib.stream_of(self.device))
+            off += x.size
+            b0 += Bk
         return out
 
     def resample_images(self, sel, start_x=-150, end_x=0):
@@ -209,9 +253,7 @@ def convergence(cache: GatherCache, max_size, bt_times, sigma, ref_freq_idx, fre
     ev = (lambda name: phases.setdefault(name, torch.cuda.Event(enable_timing=True)).record()) if phases is not None \
         else (lambda name: None)
     ev("select0")
-    stacks = torch.empty((B, e + 1 - s, plan.nt), dtype=torch.float32, device=cache.device)
-    for k, sel in enumerate(sels):
-        cache.resample_stacks(sel, start_x, end_x, out=stacks[k * bt_times:(k + 1) * bt_times])
+    stacks = cache.resample_stacks_sizes(sels, start_x, end_x)
     ev("select1")
     fv = fv_from_fk(fk_grid(stacks, plan), plan)
     ev("disp1")
@@ -221,9 +263,9 @@ def convergence(cache: GatherCache, max_size, bt_times, sigma, ref_freq_idx, fre
             for m in range(len(freq_lb))]  # every mode's walk queued, one wait below
     ev("ridge1")
     for m, pd in enumerate(pend):
-        r = ridges_finish(pd)
-        for k in range(max_size):
-            out[m, k] = np.sum(np.std(r[k * bt_times:(k + 1) * bt_times], axis=0))
+        r = np.asarray(ridges_finish(pd))
+        # per size: the std over its bt_times resamples of each frequency's pick, summed over frequencies
+        out[m] = np.std(r.reshape(max_size, bt_times, -1), axis=1).sum(axis=1)
     return out
 
 

@@ -92,6 +92,23 @@ def test_resample_stacks_and_images(device):
         assert np.abs(fv[b] - rfv).max() <= 1e-4 * np.abs(rfv).max()
 
 
+def test_resample_stacks_sizes_equal_per_size(device):
+    """resample_stacks_sizes (convergence's one upload + one select_mean launch per size) equals resample_stacks
+    called per size, row for row, including sizes of one pass and repeated passes."""
+    import torch
+
+    from das_diff_veh_amd import bootstrap as bt
+    wins, _ = _windows()
+    cache = bt.GatherCache(wins, **KW)
+    rng = np.random.default_rng(5)
+    sels = [rng.integers(0, cache.n, size=(3, k)).astype(np.int32) for k in (1, 2, 4, 3)]
+    got = cache.resample_stacks_sizes(sels)
+    want = torch.cat([cache.resample_stacks(x) for x in sels])
+    assert torch.equal(got, want)
+    with pytest.raises(ValueError):
+        cache.resample_stacks_sizes([np.array([[0, cache.n]], np.int32)])
+
+
 def _pick_parity(dev_picks, ref_picks, ref_fv_band, dev_fv_band, vels):
     """Raw ridge picks (one velocity per band column): the device's must equal the reference's in every
     column, except at a float tie the two images' own measured discrepancy allows: the device's pick is
