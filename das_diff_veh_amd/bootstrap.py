@@ -81,10 +81,11 @@ def ridges_launch(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25
         raise ValueError("the frequency band must be contiguous")
     c0, nb = int(band[0]), int(band.size)
     dev = fv.device
-    vref = None
+    from .device import upload
+    vr = None
     if ref_freq_idx is not None and ref_vel is not None:
         vr = ref_vel(freqs[band]) if callable(ref_vel) else np.asarray(ref_vel, dtype=np.float64)
-        vref = torch.as_tensor(np.asarray(vr, dtype=np.float64).reshape(nb), device=dev)
+        vr = np.asarray(vr, dtype=np.float64).reshape(nb)
     # ref_freq_idx=None -> vel_max mode (INT32_MIN); a negative index is a Python index into the band,
     # walked in the reference's loop order (modules/utils.py:662-671)
     ref = -2 ** 31 if ref_freq_idx is None else int(ref_freq_idx)
@@ -93,8 +94,10 @@ def ridges_launch(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25
     B = fv.shape[0]
     out = torch.empty((B, nb), dtype=torch.float64, device=dev)
     status = torch.zeros(B, dtype=torch.int32, device=dev)
-    vel_t = torch.as_tensor(vel_desc, device=dev)
-    sg = torch.as_tensor(_sg_ridge(), device=dev)
+    # the walk's host tables in one asynchronous copy: the launch is queued without waiting for the work before it
+    tabs = upload([vel_desc, np.asarray(_sg_ridge(), dtype=np.float64)] + ([vr] if vr is not None else []), dev)
+    vel_t, sg = tabs[0], tabs[1]
+    vref = tabs[2] if vr is not None else None
     picks = torch.empty((B, nb), dtype=torch.float64, device=dev) if return_picks else None
     _lib.call("dvh_ridge", _lib.ptr(fv), fv.stride(0), B, fv.shape[1], fv.shape[2], c0, nb, _lib.ptr(vel_t), ref,
               float(sigma), float(vel_max), _lib.ptr(vref), _lib.ptr(sg), 25, _lib.ptr(out), _lib.ptr(status),
@@ -103,6 +106,15 @@ def ridges_launch(fv, freqs, vels, freq_lb, freq_ub, ref_freq_idx=None, sigma=25
 
 
 _DISP_PLANS = {}  # (nch, w, dt, freqs, vels) -> DispPlan, shared by GatherCache instances
+_STREAMS = {}
+
+
+def _side_stream(device, k):
+    """The k-th side stream of a device (created once)."""
+    key = (str(device), k)
+    if key not in _STREAMS:
+        _STREAMS[key] = torch.cuda.Stream(device=device)
+    return _STREAMS[key]
 
 
 class GatherCache:
@@ -258,9 +270,24 @@ def convergence(cache: GatherCache, max_size, bt_times, sigma, ref_freq_idx, fre
     fv = fv_from_fk(fk_grid(stacks, plan), plan)
     ev("disp1")
     out = np.empty((len(freq_lb), max_size))
-    pend = [ridges_launch(fv, FREQS, VELS, freq_lb[m], freq_up[m], ref_freq_idx=ref_freq_idx[m] -
-                          int(np.sum(FREQS < freq_lb[m])), sigma=sigma[m], vel_max=800, ref_vel=ref_vel[m])
-            for m in range(len(freq_lb))]  # every mode's walk queued, one wait below
+    # every mode's walk queued at once, each on its own stream: one walk is one wave per resample (1 800 waves,
+    # a fraction of the chip), so the modes run side by side; one wait below
+    main = torch.cuda.current_stream(cache.device)
+    ready = torch.cuda.Event()
+    ready.record(main)
+    pend = []
+    for m in range(len(freq_lb)):
+        st = _side_stream(cache.device, m)
+        st.wait_event(ready)
+        with torch.cuda.stream(st):
+            pend.append(ridges_launch(fv, FREQS, VELS, freq_lb[m], freq_up[m], ref_freq_idx=ref_freq_idx[m] -
+                                      int(np.sum(FREQS < freq_lb[m])), sigma=sigma[m], vel_max=800,
+                                      ref_vel=ref_vel[m]))
+            for t in pend[-1]:
+                if t is not None:
+                    t.record_stream(main)
+        fv.record_stream(st)
+        main.wait_stream(st)
     ev("ridge1")
     for m, pd in enumerate(pend):
         r = np.asarray(ridges_finish(pd))
