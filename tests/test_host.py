@@ -475,3 +475,34 @@ def test_rows_of_staged_batch():
     a1.gather_x_axis[0] = 7.0
     assert own[1] is a1 and own[0].gather_x_axis[0] == 0.0 and ax.gather_x_axis[0] == 0.0
     assert len(list(own)) == 3 and own[-1] is own[2] and [a is b for a, b in zip(own[0:2], own[0:2])] == [True, True]
+
+
+def test_trajectory_packing_and_host_status(monkeypatch):
+    """plan.pack_trajectories_checked on the host (the upload stubbed): each row is its trajectory sorted as
+    interp1d's stable mergesort, zero padded, and its status is 1 exactly when fewer than 2 points remain
+    strictly ascending after the sort (repeats and NaN included) -- the rule dvh_pass_geometry applies."""
+    from das_diff_veh_amd import device, plan
+    monkeypatch.setattr(device, "upload", lambda arrs, dev: [np.asarray(a) for a in arrs])
+    rng = np.random.default_rng(0)
+    trks = []
+    for i in range(200):
+        k = int(rng.integers(0, 25))
+        x = np.sort(rng.uniform(0, 100, k))
+        if i % 7 == 0:
+            x = x[::-1].copy()
+        if i % 11 == 0 and k > 3:
+            x[2] = x[1]
+        if i % 13 == 0 and k > 3:
+            x[3] = np.nan
+        if i % 17 == 0:
+            x = rng.permutation(x)
+        trks.append((x, rng.uniform(0, 5, k)))
+    for group in (trks, [t for t in trks if len(t[0]) == 9] or trks[:1]):  # mixed lengths; one length
+        (tx, tt, ln), bad = plan.pack_trajectories_checked(group, "cpu")
+        for i, (vx, vt) in enumerate(group):
+            k = len(vx)
+            o = np.argsort(vx, kind="stable")
+            sx = vx[o]
+            assert np.array_equal(tx[i, :k], sx, equal_nan=True) and np.array_equal(tt[i, :k], vt[o])
+            assert not np.any(tx[i, k:]) and ln[i] == k
+            assert bad[i] == int(k < 2 or not np.all(sx[1:] > sx[:-1]))
