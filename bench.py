@@ -557,19 +557,69 @@ def step(job, world, ev=None, fused=True):
     fv_from_fk(fk_grid(job.stack[:, a:e, :], job.disp), job.disp, out=job.fv)
 
 
+def host_cores():
+    """The host cores this process may use: the affinity mask and, where a cgroup caps the CPU time (the GPU box
+    gives each GPU a share of a large machine), the cap in whole cores.  `usable` = the smaller; the all-core
+    CPU-baseline legs start that many single-threaded workers."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):  # cgroup v2: "<quota> <period>" or "max <period>"
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, -(-int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, -(-q // per))
+        except (OSError, ValueError):
+            pass
+    usable = min(aff, quota) if quota else aff
+    return {"affinity": aff, "cgroup_quota_cores": quota, "usable": usable, "os_cpu_count": os.cpu_count()}
+
+
+def run_cpu_workers(kind, arrays, params, budget_s, workers):
+    """`workers` single-threaded processes of oracle/cpu_legs.py KIND (no GPU state), all at once for budget_s
+    each, over a sample saved as memory-mapped .npy files; returns their result dicts (a worker that fails or
+    hangs does not count)."""
+    import tempfile
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    res = []
+    with tempfile.TemporaryDirectory() as d:
+        for k, v in arrays.items():
+            np.save(os.path.join(d, k + ".npy"), np.ascontiguousarray(v))
+        with open(os.path.join(d, "params.json"), "w") as fh:
+            json.dump(params, fh)
+        procs = [subprocess.Popen([sys.executable, "-m", "oracle.cpu_legs", kind, d, str(w), str(budget_s)], cwd=ROOT,
+                                  env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+                 for w in range(workers)]
+        for pr in procs:
+            try:
+                out, _ = pr.communicate(timeout=budget_s * 6 + 180)
+                res.append(json.loads(out.strip().splitlines()[-1]))
+            except Exception:
+                pr.kill()
+    if not res:
+        raise RuntimeError(f"no CPU-baseline worker ({kind}) finished")
+    return res
+
+
 def cpu_baseline(job, budget_s=20.0, workers=None):
     """Reference-structured CPU path (oracle/ref_loop.py) on a bounded sample of the same windows.
 
-    1 core: the bench windows themselves (host copies) for about budget_s / 2, plus one f-v image
-    per pivot set.  All cores: `workers` single-threaded processes (spawned, no GPU state; the box's
-    CPU share is 16) each looping over a saved sample of the windows for budget_s / 2; the value is
-    the aggregate windows/s, extrapolated with the 1-core image cost to one full step."""
-    import subprocess
-    import tempfile
-
+    1 core: the bench windows themselves (host copies) for about budget_s / 2, plus one f-v image per pivot set.
+    All cores: one single-threaded process per usable host core (host_cores(): affinity mask, cgroup cap), each
+    looping over a saved sample of the windows for budget_s / 2 and then imaging its stack (oracle/cpu_legs.py
+    vsg); windows/s and images/s are both measured with every core busy, and the step's windows and class images
+    are priced at those aggregate rates."""
     from oracle import ref_loop
     torch.set_num_threads(1)
-    workers = workers or max(1, min(16, os.cpu_count() or 1))
+    cores = host_cores()
+    workers = workers or cores["usable"]
     n_win, t_win, t_img, n_img = 0, 0.0, 0.0, 0
     t_start = time.time()
     one_budget = budget_s / 2
@@ -603,34 +653,23 @@ def cpu_baseline(job, budget_s=20.0, workers=None):
     total_images = job.stack.shape[0]
     rate1 = total_windows / (per_window * total_windows + per_image * total_images)
     host, x_axis, t_axis, trk, prm = samples[0]
-    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
-    with tempfile.TemporaryDirectory() as d:
-        path = os.path.join(d, "sample.npz")
-        np.savez(path, wins=host, x_axis=x_axis, t_axis=t_axis, vx=np.stack([v for v, _ in trk]),
-                 vt=np.stack([t for _, t in trk]), pivot=prm.pivot, start_x=prm.start_x, end_x=prm.end_x)
-        procs = [subprocess.Popen([sys.executable, "-m", "oracle.ref_loop", path, str(w), str(budget_s / 2)],
-                                  cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
-                 for w in range(workers)]
-        res = []
-        for pr in procs:
-            try:
-                out, _ = pr.communicate(timeout=budget_s * 4 + 120)
-                done, secs = out.split()
-                res.append((int(done), float(secs)))
-            except Exception:  # a worker that failed or hung does not count
-                pr.kill()
-    if not res:
-        raise RuntimeError("no CPU-baseline worker finished")
-    workers = len(res)
-    agg_window_rate = sum(n / t for n, t in res)
-    step_s = total_windows / agg_window_rate + per_image * total_images / workers
-    return dict(value=total_windows / step_s, unit="vehicle-pass windows/s", cores=workers, kind="port",
-                sample=f"all cores: {workers} single-threaded processes x {budget_s / 2:.0f} s over {host.shape[0]} "
-                       f"saved windows, {sum(n for n, _ in res)} windows (VSG two-sided), f-v images at the 1-core "
-                       f"cost / {workers}; 1 core: {n_win} windows ({per_window * 1e3:.1f} ms/window), {n_img} f-v "
-                       f"images ({per_image * 1e3:.1f} ms/image) -> {rate1:.2f} windows/s; the port leaves out the "
-                       f"reference's per-__add__ deepcopy of the window (apis/virtual_shot_gather.py:196), so the "
-                       f"reference itself is slower; cpu={platform.processor() or platform.machine()}",
+    res = run_cpu_workers("vsg", dict(wins=host, x_axis=x_axis, t_axis=t_axis, vx=np.stack([v for v, _ in trk]),
+                                      vt=np.stack([t for _, t in trk])),
+                          dict(pivot=prm.pivot, start_x=prm.start_x, end_x=prm.end_x), budget_s / 2, workers)
+    win_rate = sum(r["windows"] / r["secs"] for r in res)
+    img_rate = sum(r["images"] / r["img_secs"] for r in res)
+    step_s = total_windows / win_rate + total_images / img_rate
+    return dict(value=total_windows / step_s, unit="vehicle-pass windows/s", cores=len(res), kind="port",
+                host_cores=cores,
+                sample=f"all cores: {len(res)} single-threaded processes (usable cores: affinity {cores['affinity']}, "
+                       f"cgroup cap {cores['cgroup_quota_cores']}), each {budget_s / 2:.0f} s of VSG gathers over "
+                       f"{host.shape[0]} saved windows ({sum(r['windows'] for r in res)} windows, two-sided) then f-v "
+                       f"images of its stack ({sum(r['images'] for r in res)} images), both rates measured with every "
+                       f"core busy: {win_rate:.2f} windows/s, {img_rate:.1f} images/s; 1 core: {n_win} windows "
+                       f"({per_window * 1e3:.1f} ms/window), {n_img} f-v images ({per_image * 1e3:.1f} ms/image) -> "
+                       f"{rate1:.2f} windows/s; the port leaves out the reference's per-__add__ deepcopy of the window "
+                       f"(apis/virtual_shot_gather.py:196), so the reference itself is slower; "
+                       f"cpu={platform.processor() or platform.machine()}",
                 value_1core=rate1)
 
 
@@ -638,12 +677,13 @@ def cpu_baseline_sliding(job, budget_s=20.0, workers=None):
     """configs[3] CPU path: oracle/ref_loop.gather (the reference's VirtualShotGather loop, including its
     data / ||data||_F of the whole 4,096 x 8,192 window per call) for sample units of the bench's first
     batch, each at its own pivot (start_x / end_x = pivot -/+ 200 m), on host copies of their windows.
-    1 core over the sample for budget_s / 2, then `workers` single-threaded processes for budget_s / 2;
-    passes/s = units/s / (units per pass), with the f-v images at the 1-core cost / workers."""
-    import tempfile
+    1 core over the sample for budget_s / 2, then one single-threaded process per usable host core for budget_s / 2
+    (oracle/cpu_legs.py vsg: units, then f-v images of the worker's stack, both measured with every core busy);
+    passes/s = units/s / (units per pass), with the step's images at the measured aggregate image rate."""
     from oracle import ref_loop
     torch.set_num_threads(1)
-    workers = workers or max(1, min(16, os.cpu_count() or 1))
+    cores = host_cores()
+    workers = workers or cores["usable"]
     cu = job.cpu_units
     x_axis, t_axis, pch, trk, plan, half = (cu[k] for k in ("x_axis", "t_axis", "pch", "trk", "plan", "half"))
     ns = min(4, plan.n_pass)
@@ -669,37 +709,26 @@ def cpu_baseline_sliding(job, budget_s=20.0, workers=None):
     upp = cu["units_per_pass"]
     n_img = job.stack.shape[0]
     rate1 = job.n_global / (per_unit * upp * job.n_global + per_image * n_img)
-    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
-    res = []
-    with tempfile.TemporaryDirectory() as d:
-        path = os.path.join(d, "sample.npz")
-        qs = [int(plan.unit_window[u]) for u in units]
-        pv = np.array([float(x_axis[pch[int(plan.unit_pivot[u])]]) for u in units])
-        np.savez(path, wins=np.stack([hosts[q].astype(np.float32) for q in qs[:2]]), x_axis=x_axis, t_axis=t_axis,
-                 vx=np.stack([trk[q][0] for q in qs[:2]]), vt=np.stack([trk[q][1] for q in qs[:2]]), pivot=pv[:2],
-                 start_x=pv[:2] - half, end_x=pv[:2] + half)
-        procs = [subprocess.Popen([sys.executable, "-m", "oracle.ref_loop", path, str(wk), str(budget_s / 2)],
-                                  cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
-                 for wk in range(workers)]
-        for pr in procs:
-            try:
-                out, _ = pr.communicate(timeout=budget_s * 6 + 120)
-                done, secs = out.split()
-                res.append((int(done), float(secs)))
-            except Exception:  # a worker that failed or hung does not count
-                pr.kill()
-    if not res:
-        raise RuntimeError("no CPU-baseline worker finished")
-    unit_rate = sum(n / t for n, t in res)
-    step_s = job.n_global * upp / unit_rate + per_image * n_img / len(res)
+    qs = [int(plan.unit_window[u]) for u in units]
+    pv = np.array([float(x_axis[pch[int(plan.unit_pivot[u])]]) for u in units])
+    res = run_cpu_workers("vsg", dict(wins=np.stack([hosts[q].astype(np.float32) for q in qs[:2]]), x_axis=x_axis,
+                                      t_axis=t_axis, vx=np.stack([trk[q][0] for q in qs[:2]]),
+                                      vt=np.stack([trk[q][1] for q in qs[:2]]), pivot=pv[:2], start_x=pv[:2] - half,
+                                      end_x=pv[:2] + half), {}, budget_s / 2, workers)
+    unit_rate = sum(r["windows"] / r["secs"] for r in res)
+    img_rate = sum(r["images"] / r["img_secs"] for r in res)
+    step_s = job.n_global * upp / unit_rate + n_img / img_rate
     return dict(value=job.n_global / step_s, unit="vehicle-pass windows/s", cores=len(res), kind="port",
-                sample=f"all cores: {len(res)} single-threaded processes x {budget_s / 2:.0f} s, "
-                       f"{sum(n for n, _ in res)} (pass, pivot) units of 2 saved 4,096 x 8,192 windows (VSG two-sided, "
-                       f"+-{half:.0f} m at each unit's pivot); {upp:.2f} units per pass; f-v images at the 1-core cost / "
-                       f"{len(res)}; 1 core: {n_u} units ({per_unit * 1e3:.0f} ms/unit, the window's data / ||data|| "
-                       f"included), f-v image {per_image * 1e3:.1f} ms -> {rate1:.3f} passes/s; without the "
-                       f"reference's per-__add__ deepcopy (apis/virtual_shot_gather.py:196); "
-                       f"cpu={platform.processor() or platform.machine()}",
+                host_cores=cores,
+                sample=f"all cores: {len(res)} single-threaded processes (usable cores: affinity {cores['affinity']}, "
+                       f"cgroup cap {cores['cgroup_quota_cores']}) x {budget_s / 2:.0f} s, "
+                       f"{sum(r['windows'] for r in res)} (pass, pivot) units of 2 saved 4,096 x 8,192 windows (VSG "
+                       f"two-sided, +-{half:.0f} m at each unit's pivot), then f-v images of each worker's stack "
+                       f"({sum(r['images'] for r in res)}), both rates with every core busy: {unit_rate:.2f} units/s, "
+                       f"{img_rate:.1f} images/s; {upp:.2f} units per pass; 1 core: {n_u} units "
+                       f"({per_unit * 1e3:.0f} ms/unit, the window's data / ||data|| included), f-v image "
+                       f"{per_image * 1e3:.1f} ms -> {rate1:.3f} passes/s; without the reference's per-__add__ deepcopy "
+                       f"(apis/virtual_shot_gather.py:196); cpu={platform.processor() or platform.machine()}",
                 value_1core=rate1)
 
 
@@ -849,7 +878,7 @@ def timelapse_main(args, world, rank, device):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the oracle's map_fv (fft2, FITPACK bilinear via RectBivariateSpline, savgol) on one core over a
-        # bounded sample of the same gathers
+        # bounded sample of the same gathers, then on every usable core at once (oracle/cpu_legs.py fv)
         budget = args.cpu_budget / 2
         torch.set_num_threads(1)
         n, t_c = 0, time.time()
@@ -857,8 +886,16 @@ def timelapse_main(args, world, rank, device):
             odisp.map_fv(host[n], dx, dt, freqs, vels)
             n += 1
         secs = time.time() - t_c
-        res["cpu_baseline"] = {"value": n / secs, "unit": "f-v images/s", "cores": 1, "kind": "port",
-                               "sample": f"oracle/disp.py map_fv on {n} of the bench gathers in {secs:.1f} s, one core, "
+        cores = host_cores()
+        wres = run_cpu_workers("fv", dict(gathers=host[:16], freqs=freqs, vels=vels), dict(dx=dx, dt=dt), budget,
+                               cores["usable"])
+        rate = sum(r["images"] / r["secs"] for r in wres)
+        res["cpu_baseline"] = {"value": rate, "unit": "f-v images/s", "cores": len(wres), "kind": "port",
+                               "host_cores": cores, "value_1core": n / secs,
+                               "sample": f"oracle/disp.py map_fv: all cores: {len(wres)} single-threaded processes x "
+                                         f"{budget:.0f} s over 16 of the bench gathers ({sum(r['images'] for r in wres)} "
+                                         f"images; usable cores: affinity {cores['affinity']}, cgroup cap "
+                                         f"{cores['cgroup_quota_cores']}); 1 core: {n} gathers in {secs:.1f} s; "
                                          f"cpu={platform.processor() or platform.machine()}"}
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
     if rank == 0:
@@ -955,7 +992,8 @@ def prep_main(args, world, rank, device):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the oracle (scipy's sosfiltfilt + the reference's imputation / norm) on one core, on trace slices of the
-        # same record for ~cpu_budget / 2 s, scaled to the full record
+        # same record for ~cpu_budget / 2 s, scaled to the full record; then every usable core at once, each worker
+        # on its own 64-trace slice (oracle/cpu_legs.py prep)
         torch.set_num_threads(1)
         sub = host[:128]
         n, t_c = 0, time.time()
@@ -963,11 +1001,19 @@ def prep_main(args, world, rank, device):
             oprep.surface_wave_prep(sub, dt, scipy_filter=True)
             n += 1
         secs = (time.time() - t_c) / n
-        res["cpu_baseline"] = {"value": sub.shape[0] / n_ch / secs, "unit": "records/s", "cores": 1, "kind": "port",
+        cores = host_cores()
+        wres = run_cpu_workers("prep", dict(record=host[128:192]), dict(dt=dt), args.cpu_budget / 2, cores["usable"])
+        rate = sum(r["rows"] / r["secs"] for r in wres) / n_ch
+        res["cpu_baseline"] = {"value": rate, "unit": "records/s", "cores": len(wres), "kind": "port",
+                               "host_cores": cores, "value_1core": sub.shape[0] / n_ch / secs,
                                "sample": f"the reference's path (scipy.signal.sosfiltfilt as bandpass_data calls it + "
-                                         f"oracle/preprocess.py's imputation and norm) on 128 of the record's traces, "
-                                         f"{n} runs ({secs * 1e3:.0f} ms each), scaled x {n_ch // 128} to the 1,024-trace "
-                                         f"record; cpu={platform.processor() or platform.machine()}"}
+                                         f"oracle/preprocess.py's imputation and norm): all cores: {len(wres)} "
+                                         f"single-threaded processes x {args.cpu_budget / 2:.0f} s, each on a 64-trace "
+                                         f"slice of the record ({sum(r['rows'] for r in wres)} traces; usable cores: "
+                                         f"affinity {cores['affinity']}, cgroup cap {cores['cgroup_quota_cores']}), "
+                                         f"traces/s / {n_ch}; 1 core: 128 traces, {n} runs ({secs * 1e3:.0f} ms each), "
+                                         f"scaled x {n_ch // 128} to the 1,024-trace record; "
+                                         f"cpu={platform.processor() or platform.machine()}"}
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -1097,11 +1143,26 @@ def bootstrap_main(args, world, rank, device):
         per_g = tg / ng
         windows_drawn = T * S * (S + 1) // 2
         cpu_s = windows_drawn * per_g + B * (t_img + t_rdg)
-        res["cpu_baseline"] = {"value": B / cpu_s, "unit": "resamples/s", "cores": 1, "kind": "port",
-                               "sample": f"oracle on one core: {ng} VSG gathers ({per_g * 1e3:.1f} ms each, "
-                                         f"oracle/ref_loop.py), one f-v image ({t_img * 1e3:.1f} ms, map_fv) and 4 "
-                                         f"ridges ({t_rdg * 1e3:.1f} ms), priced over the step: {windows_drawn} gathers "
-                                         f"(the reference recomputes every resample's gathers) + {B} images + ridges; "
+        # every usable core at once: each worker prices the same step from its own measured pieces
+        cores = host_cores()
+        pts = [None] + [[list(map(float, c.x)), list(map(float, c.y))] for c in curves[1:]]
+        wres = run_cpu_workers("boot", dict(wins=host.astype(np.float32), x_axis=x_axis, t_axis=t_axis,
+                                            vx=np.stack([trk[i][0] for i in range(host.shape[0])]),
+                                            vt=np.stack([trk[i][1] for i in range(host.shape[0])])),
+                               dict(pivot=700.0, start_x=500.0, end_x=900.0, sigma=sigma, ref_idx=ref_idx, lb=lb, ub=ub,
+                                    curves=pts), args.cpu_budget / 2, cores["usable"])
+        rate = sum(B / (windows_drawn * r["g_secs"] / r["gathers"] + B * (r["img_secs"] + r["ridge_secs"]))
+                   for r in wres)
+        res["cpu_baseline"] = {"value": rate, "unit": "resamples/s", "cores": len(wres), "kind": "port",
+                               "host_cores": cores, "value_1core": B / cpu_s,
+                               "sample": f"oracle, all cores: {len(wres)} single-threaded processes (usable cores: "
+                                         f"affinity {cores['affinity']}, cgroup cap {cores['cgroup_quota_cores']}), each "
+                                         f"timing VSG gathers for {0.7 * args.cpu_budget / 2:.0f} s "
+                                         f"({sum(r['gathers'] for r in wres)} in all), one f-v image and 4 ridges, every "
+                                         f"core busy, and pricing the step: {windows_drawn} gathers (the reference "
+                                         f"recomputes every resample's gathers) + {B} images + ridges; 1 core: {ng} VSG "
+                                         f"gathers ({per_g * 1e3:.1f} ms each, oracle/ref_loop.py), one f-v image "
+                                         f"({t_img * 1e3:.1f} ms, map_fv) and 4 ridges ({t_rdg * 1e3:.1f} ms); "
                                          f"cpu={platform.processor() or platform.machine()}"}
         res["speedup_vs_cpu"] = res["value"] / res["cpu_baseline"]["value"]
     if rank == 0:

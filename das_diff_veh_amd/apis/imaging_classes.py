@@ -1,4 +1,4 @@
-"""Per-class imaging orchestration — drop-in for apis/imaging_classes.py:8-48, 87-141 of the reference.
+"""Per-class imaging orchestration — drop-in for apis/imaging_classes.py:8-141 of the reference.
 
 ``get_images`` no longer loops over passes in Python: every window of the list goes to the device in
 one batch, the class mean is produced by the fused correlate-and-stack kernel
@@ -9,6 +9,8 @@ resample as one device batch over gathers computed once (das_diff_veh_amd.bootst
 from __future__ import annotations
 
 import copy
+import logging
+import random
 
 import numpy as np
 
@@ -60,10 +62,20 @@ class ImagesFromWindows:
         self.avg_image = sum(self.images)
         self.avg_image = self.avg_image / len(self.images)
 
+    def save_images(self, fig_folder, file_prefix):
+        """apis/imaging_classes.py:110-117: one figure per image and one of the mean, by the images' plot_image
+        (plotting is outside the accelerated path: the image classes' plot_image raises with a pointer)."""
+        for k, image in enumerate(self.images):
+            image.plot_image(f"{file_prefix}{k}.png", norm=True, fig_folder=fig_folder)
+        self.avg_image.plot_image(f"{file_prefix}_avg.png", norm=True, fig_folder=fig_folder)
+
 
 class DispersionImagesFromWindows(ImagesFromWindows):
     def __init__(self, windows, image_cls=SurfaceWaveDispersion):
         super().__init__(windows, image_cls)
+
+    def save_images(self, fig_folder, file_prefix="veh_disp"):
+        super().save_images(fig_folder, file_prefix)
 
     def get_images(self, norm=False, mute_offset=300, mute=True, shard_over_ranks=False, group=None,
                    **imaging_kwargs):
@@ -144,6 +156,40 @@ class VirtualShotGathersFromWindows(ImagesFromWindows):
         avg = stack[0].detach().to("cpu").numpy().astype(np.float64)
         self.avg_image = VirtualShotGather._from_arrays(windows[0], avg, geoms[0].gather_x_axis,
                                                         geoms[0].gather_t_axis)
+
+    def save_images(self, fig_folder, file_prefix="veh_vshot"):
+        super().save_images(fig_folder, file_prefix)
+
+
+_log = logging.getLogger(__name__)
+
+
+def save_disp_imgs(windows, weight, min_win, x, start_x, end_x, offset, fig_dir):
+    """apis/imaging_classes.py:50-85 (imaging_diff_{speed,weight}.ipynb#cell21): the class stack of a random
+    subset of min_win windows and its dispersion image.
+
+    Same draw as the reference: ``random.sample(range(len(windows)), min_win)`` on Python's module-level
+    generator (so a notebook's ``random.seed`` gives the same subset), the subset taken in window order
+    (``i in sel_idx``), ``get_images(pivot=x, start_x, end_x, wlen=2, include_other_side=True)`` -- one device
+    batch through the fused correlate-and-stack kernel -- and ``compute_disp_image(end_x=0, start_x=-offset)``.
+    The return value is the reference's: ``images_all``, the VirtualShotGathersFromWindows of ALL windows on which
+    get_images was never called (:56, :85).  The imaged subset stays reachable as ``images_all.selected`` (its
+    ``avg_image.XCF_out`` / ``avg_image.disp.fv_map``) and the draw as ``images_all.sel_idx``, attributes the
+    reference does not have.  Not done (plotting is outside the accelerated path): the figures the reference
+    writes under ``fig_dir/x/`` (plot_image of the stack, plot_fv_map with and without normalisation) and the
+    CLAHE enhancement (fv_map_enhance, cv2), whose result the reference only passes to a commented-out plot."""
+    image_from_window_cls = VirtualShotGathersFromWindows
+    sel_idx = random.sample(range(len(windows)), min_win)
+    images_all = image_from_window_cls(windows)
+    chosen = set(sel_idx)
+    _images = image_from_window_cls([e for i, e in enumerate(windows) if i in chosen])
+    _images.get_images(pivot=x, start_x=start_x, end_x=end_x, wlen=2, include_other_side=True)
+    _log.info("save_disp_imgs: figures sg_%s_cars.pdf / disp_%s_cars_no_norm.pdf / disp_%s_cars_no_enhance.pdf under "
+              "%s/%s/ are not written (plotting is outside the accelerated path; plot images.selected.avg_image with "
+              "the reference's plot_xcorr / plot_fv_map)", weight, weight, weight, fig_dir, x)
+    _images.avg_image.compute_disp_image(end_x=0, start_x=-offset)
+    images_all.selected, images_all.sel_idx = _images, sel_idx
+    return images_all
 
 
 def bootstrap_disp(surf_wins, bt_size, bt_times, sigma, pivot, start_x, end_x, ref_freq_idx, freq_lb, freq_up,

@@ -39,11 +39,12 @@ void stream_copy(char* d, const char* s, int64_t nbytes) {
 }  // namespace
 
 DVH_API int dvh_host_gather(void* dst, const void* const* src, int64_t nbytes, int32_t n) {
-  if ((!dst || !src) && n > 0) return 1;
-  if (nbytes < 0 || n < 0) return 1;
+  if ((!dst || !src) && n > 0) return dvh::set_error(-2, "null pointer argument");
+  if (nbytes < 0 || n < 0) return dvh::set_error(-2, "negative size or count");
+  for (int32_t i = 0; i < n; ++i)
+    if (!src[i]) return dvh::set_error(-2, "null source window");
   char* d = static_cast<char*>(dst);
   for (int32_t i = 0; i < n; ++i) {
-    if (!src[i]) return 1;
     stream_copy(d + (int64_t)i * nbytes, static_cast<const char*>(src[i]), nbytes);
   }
   _mm_sfence();  // the streaming stores are globally visible before the caller issues the H2D copy

@@ -1,7 +1,9 @@
 """Device selection and host<->device staging for the drop-in API (PyTorch is plumbing only)."""
 from __future__ import annotations
 
+import atexit
 import os
+import threading
 
 import numpy as np
 import torch
@@ -19,19 +21,47 @@ def default_device():
 # of chunk k + 1 runs while chunk k crosses PCIe.
 STAGE_BYTES = int(os.environ.get("DVH_STAGE_MB", "64")) << 20  # 64 MB: 36.2-36.3 k vs 35.0-35.4 k windows/s at 128
 _STAGE = {}
+# One staging at a time per (device, dtype): the pinned and device chunk buffers are shared by every caller (the
+# background thread of stage_async and the caller's own to_device_f32), so a staging holds its stager's lock from
+# its first host copy to its last H2D issue.
+_STAGE_LOCK = threading.Lock()
 
 
 def _stager(device, dtype, nbytes):
-    """(side stream, two pinned host buffers, two device buffers, two events) for chunks of <= nbytes."""
+    """(side stream, two pinned host buffers, two device buffers, two events, lock) for chunks of <= nbytes.
+    A stager that must grow first drains its side stream (the old buffers' copies are done before they are
+    dropped); its device buffers are allocated on the side stream, the only stream that touches them."""
     key = (str(device), str(dtype))
-    st = _STAGE.get(key)
-    if st is None or st["nbytes"] < nbytes:
-        st = dict(nbytes=nbytes, stream=torch.cuda.Stream(device=device),
-                  pinned=[torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)],
-                  dev=[torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(2)],
-                  free=[torch.cuda.Event() for _ in range(2)])
-        _STAGE[key] = st
+    with _STAGE_LOCK:
+        st = _STAGE.get(key)
+        if st is None:
+            st = dict(nbytes=0, stream=torch.cuda.Stream(device=device), lock=threading.Lock(),
+                      free=[torch.cuda.Event() for _ in range(2)])
+            _STAGE[key] = st
     return st
+
+
+def _grow(st, device, nbytes):
+    """Called with st['lock'] held: buffers of >= nbytes (at least STAGE_BYTES, so they are sized once)."""
+    if st["nbytes"] >= nbytes:
+        return
+    st["stream"].synchronize()  # the copies that read or write the old buffers are done
+    nb = max(nbytes, STAGE_BYTES)
+    st["pinned"] = [torch.empty(nb, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    with torch.cuda.stream(st["stream"]):
+        st["dev"] = [torch.empty(nb, dtype=torch.uint8, device=device) for _ in range(2)]
+    st["nbytes"] = nb
+
+
+def sync_staging():
+    """Wait for every staging side stream's queued copies (process exit, tests)."""
+    with _STAGE_LOCK:
+        sts = [v for k, v in _STAGE.items() if isinstance(k, tuple)]
+    for st in sts:
+        st["stream"].synchronize()
+
+
+atexit.register(lambda: sync_staging() if torch.cuda.is_initialized() else None)
 
 
 import ctypes  # noqa: E402
@@ -45,9 +75,10 @@ STAGE_RAMP = int(os.environ.get("DVH_STAGE_RAMP", "0"))  # 0: off, r: first chun
 
 def _pool():
     import concurrent.futures as cf
-    if "pool" not in _STAGE:
-        _STAGE["pool"] = cf.ThreadPoolExecutor(_NTHREADS)
-    return _STAGE["pool"]
+    with _STAGE_LOCK:
+        if "pool" not in _STAGE:
+            _STAGE["pool"] = cf.ThreadPoolExecutor(_NTHREADS)
+        return _STAGE["pool"]
 
 
 def stage_windows(hosts, device, out=None, wait=True):
@@ -66,6 +97,12 @@ def stage_windows(hosts, device, out=None, wait=True):
     per = int(np.prod(shape)) * np.dtype(src).itemsize
     k = max(1, min(n, STAGE_BYTES // max(per, 1)))
     st = _stager(device, src, k * per)
+    with st["lock"]:
+        _grow(st, device, k * per)
+        return _stage_chunks(hosts, st, out, n, shape, src, per, k, device, wait)
+
+
+def _stage_chunks(hosts, st, out, n, shape, src, per, k, device, wait):
     pool = _pool()
     tdt = torch.float32 if src == np.float32 else torch.float64
     # chunk starts: with STAGE_RAMP = r the first chunks are k / r, 2 k / r, ... windows, so that the first H2D
@@ -109,6 +146,10 @@ def stage_windows(hosts, device, out=None, wait=True):
                 d.copy_(pin, non_blocking=True)
                 out[a:a + kk].copy_(d)
             st["free"][b].record(st["stream"])
+    # `out` may come from another stream's pool (stage_async allocates it on the caller's stream): the allocator
+    # must not hand its memory out again before the side stream's copies into it are done, even if the caller
+    # drops it without waiting (an exception between staging and launch)
+    out.record_stream(st["stream"])
     done = torch.cuda.Event()
     done.record(st["stream"])
     if wait:
@@ -119,19 +160,36 @@ def stage_windows(hosts, device, out=None, wait=True):
 
 def stage_async(hosts, device):
     """stage_windows on a background thread: the host copies overlap the caller's own host work (e.g. the batch's
-    tables).  Returns a function that yields the device tensor, the current stream made to wait for it."""
+    tables).  Returns a _Staged: calling it yields the device tensor, the current stream made to wait for it."""
     import concurrent.futures as cf
-    if "bg" not in _STAGE:
-        _STAGE["bg"] = cf.ThreadPoolExecutor(1)
+    with _STAGE_LOCK:
+        if "bg" not in _STAGE:
+            _STAGE["bg"] = cf.ThreadPoolExecutor(1)
     n = len(hosts)
     out = torch.empty((n,) + tuple(hosts[0].shape), dtype=torch.float32, device=device)  # caller's stream
     fut = _STAGE["bg"].submit(stage_windows, hosts, device, out, False)
+    return _Staged(fut, device)
 
-    def result():
-        t, ev = fut.result()
-        torch.cuda.current_stream(device).wait_event(ev)
+
+class _Staged:
+    """A staging in flight: call it for the device tensor (the current stream then waits for its copies);
+    drain() waits for the host copies and the DMA without using the tensor (an abandoned staging: the pinned
+    buffers are free for the next staging and no copy writes memory the caller has released)."""
+
+    def __init__(self, fut, device):
+        self._fut, self._device = fut, device
+
+    def __call__(self):
+        t, ev = self._fut.result()
+        torch.cuda.current_stream(self._device).wait_event(ev)
         return t
-    return result
+
+    def drain(self):
+        try:
+            _, ev = self._fut.result()
+        except Exception:  # the staging's own error belongs to whoever uses the tensor
+            return
+        ev.synchronize()
 
 
 def to_device_f32(arrays, device=None):

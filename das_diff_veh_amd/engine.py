@@ -10,8 +10,11 @@ is on, and with a ||window||_F^2 launch otherwise.
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
+import os
 import sys
+import threading
 
 import numpy as np
 
@@ -170,18 +173,40 @@ def gathers(windows, prm: VsgParams, device=None):
     return res, axes
 
 
+# Opt-in (DVH_SWITCH_INTERVAL=<seconds>, default off): while any stacked() call is staging host windows, the
+# interpreter's switch interval is lowered so that the staging thread's Python steps (chunk bookkeeping between its
+# native copies) get the interpreter sooner while the calling thread groups and plans.  Process-wide state, so it is
+# reference-counted under a lock: concurrent calls restore the caller's interval only when the last one ends.
+_SWITCH = float(os.environ.get("DVH_SWITCH_INTERVAL", "0") or 0)
+_SWITCH_LOCK = threading.Lock()
+_SWITCH_STATE = {"depth": 0, "saved": None}
+
+
+@contextlib.contextmanager
+def _switch_interval():
+    if _SWITCH <= 0:
+        yield
+        return
+    with _SWITCH_LOCK:
+        if _SWITCH_STATE["depth"] == 0:
+            _SWITCH_STATE["saved"] = sys.getswitchinterval()
+            sys.setswitchinterval(min(_SWITCH_STATE["saved"], _SWITCH))
+        _SWITCH_STATE["depth"] += 1
+    try:
+        yield
+    finally:
+        with _SWITCH_LOCK:
+            _SWITCH_STATE["depth"] -= 1
+            if _SWITCH_STATE["depth"] == 0:
+                sys.setswitchinterval(_SWITCH_STATE["saved"])
+
+
 def stacked(windows, prm: VsgParams, slots=None, n_slot=1, device=None, chunk=8, counts=None):
     """Class-mean gathers [n_slot, R, w] (device tensor) over all windows, plus the gather axes.
     ``counts`` [n_slot]: the class sizes the means divide by (default: these windows' own; a rank of a
     sharded job passes the global ones, distributed.sharded_class_means)."""
-    # the staging thread's Python steps (chunk bookkeeping between its native copies) get the interpreter
-    # within ~0.2 ms instead of the default 5 ms switch interval while this thread groups and plans
-    prev = sys.getswitchinterval()
-    sys.setswitchinterval(min(prev, 2e-4))
-    try:
+    with _switch_interval():
         return _stacked(windows, prm, slots, n_slot, device, chunk, counts)
-    finally:
-        sys.setswitchinterval(prev)
 
 
 def _stacked(windows, prm, slots, n_slot, device, chunk, counts):
@@ -190,25 +215,40 @@ def _stacked(windows, prm, slots, n_slot, device, chunk, counts):
     counts = np.bincount(slots, minlength=n_slot) if counts is None else np.asarray(counts)
     # windows of one data shape (the notebooks' case) start their copies before anything else, in the caller's
     # order; a group takes its rows of the staged batch
-    early = None
-    if windows and len({np.shape(w.data) for w in windows}) == 1:
-        early = _stage(windows, range(len(windows)), device)
-    groups, axes = _groups(windows, prm)
-    if len({key[1:3] for key in groups}) != 1:
-        raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
-    if early is not None:
-        memo = {}
-        staged = [(idx, key, _rows_of(early, idx, len(windows), memo)) for key, idx in groups.items()]
-    else:  # every group's window copies start first (background thread), the tables are formed meanwhile
-        staged = [(idx, key, _stage(windows, idx, device)) for key, idx in groups.items()]
-    out = None
-    for idx, key, data_fn in staged:
-        plan = _plan(windows, idx, key, prm, device)
-        data = data_fn()
-        sched = StackSchedule(slots[idx], n_slot, chunk=chunk, counts=counts)
-        fn = vsg_stack_validated if plan.flags & 6 else vsg_stack
-        out = fn(data, plan, sched, out=out, accumulate=out is not None)
-    return out, axes
+    stagings = []  # every staging started here is waited for before an error leaves this call
+    try:
+        early = None
+        if windows and len({np.shape(w.data) for w in windows}) == 1:
+            early = _stage(windows, range(len(windows)), device)
+            stagings.append(early)
+        groups, axes = _groups(windows, prm)
+        if len({key[1:3] for key in groups}) != 1:
+            raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
+        if early is not None:
+            memo = {}
+            staged = [(idx, key, _rows_of(early, idx, len(windows), memo)) for key, idx in groups.items()]
+        else:  # every group's window copies start first (background thread), the tables are formed meanwhile
+            staged = []
+            for key, idx in groups.items():
+                staged.append((idx, key, _stage(windows, idx, device)))
+                stagings.append(staged[-1][2])
+        out = None
+        for idx, key, data_fn in staged:
+            plan = _plan(windows, idx, key, prm, device)
+            data = data_fn()
+            sched = StackSchedule(slots[idx], n_slot, chunk=chunk, counts=counts)
+            fn = vsg_stack_validated if plan.flags & 6 else vsg_stack
+            out = fn(data, plan, sched, out=out, accumulate=out is not None)
+        return out, axes
+    except BaseException:
+        # a validation error after the copies started (geometry, shapes, trajectories): the background copies
+        # finish before the error propagates, so none of them writes into memory released meanwhile and the
+        # shared pinned buffers are free for the next staging
+        for s in stagings:
+            drain = getattr(s, "drain", None)
+            if drain is not None:
+                drain()
+        raise
 
 
 def stacked_sharded(windows, prm: VsgParams, slots=None, n_slot=1, group=None, device=None, chunk=8):

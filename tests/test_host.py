@@ -506,3 +506,74 @@ def test_trajectory_packing_and_host_status(monkeypatch):
             assert np.array_equal(tx[i, :k], sx, equal_nan=True) and np.array_equal(tt[i, :k], vt[o])
             assert not np.any(tx[i, k:]) and ln[i] == k
             assert bad[i] == int(k < 2 or not np.all(sx[1:] > sx[:-1]))
+
+
+def test_abandoned_staging_is_drained(monkeypatch):
+    """engine._stacked (host logic, staging stubbed): an error raised after the window copies started -- here the
+    gather-shape check -- waits for every staging before it propagates (no copy may keep writing
+    memory the caller has released, nor the shared pinned buffers the next staging uses)."""
+    from das_diff_veh_amd import engine
+    from das_diff_veh_amd.plan import VsgParams
+
+    class FakeStaging:
+        def __init__(self):
+            self.drained = False
+
+        def __call__(self):
+            raise AssertionError("the batch must not be used after the error")
+
+        def drain(self):
+            self.drained = True
+    made = []
+
+    def fake_stage(windows, idx, device):
+        made.append(FakeStaging())
+        return made[-1]
+    monkeypatch.setattr(engine, "_stage", fake_stage)
+    wins, _ = _failing_windows()
+    wins = [wins[0], wins[4]]
+    prm = VsgParams(pivot=700, start_x=500, end_x=900, include_other_side=True, norm=False)
+    monkeypatch.setattr(engine, "_groups", lambda w, p: ({(1,) + (10, 500, 250): [0], (1,) + (11, 500, 250): [1]},
+                                                        [None, None]))
+    with pytest.raises(ValueError, match="broadcast"):
+        engine._stacked(wins, prm, None, 1, "cpu", 8, None)
+    assert len(made) == 1 and made[0].drained
+    # groups of different data shapes: one staging per group, every one drained
+    made.clear()
+    wins2 = [wins[0], engine.GatherAxes(None, None)]
+    wins2[1].data = np.zeros((3, 4), np.float32)
+    monkeypatch.setattr(engine, "_plan", lambda *a: (_ for _ in ()).throw(ValueError("bad trajectory")))
+    monkeypatch.setattr(engine, "_groups", lambda w, p: ({((60, 5500), 10, 500, 250): [0], ((3, 4), 10, 500, 250): [1]},
+                                                        [None, None]))
+    with pytest.raises(ValueError, match="bad trajectory"):
+        engine._stacked(wins2, prm, None, 1, "cpu", 8, None)
+    assert len(made) == 2 and all(m.drained for m in made)
+
+
+def test_switch_interval_is_opt_in_and_refcounted(monkeypatch):
+    """engine.stacked leaves the interpreter's switch interval alone unless DVH_SWITCH_INTERVAL asks; when asked,
+    overlapping calls restore the caller's interval only when the last one ends."""
+    import sys
+    import threading
+
+    from das_diff_veh_amd import engine
+    prev = sys.getswitchinterval()
+    monkeypatch.setattr(engine, "_SWITCH", 0.0)
+    with engine._switch_interval():
+        assert sys.getswitchinterval() == prev
+    monkeypatch.setattr(engine, "_SWITCH", 1e-4)
+    inside, go = threading.Event(), threading.Event()
+
+    def other():
+        with engine._switch_interval():
+            inside.set()
+            go.wait(5)
+    th = threading.Thread(target=other)
+    with engine._switch_interval():
+        assert sys.getswitchinterval() == pytest.approx(min(prev, 1e-4))
+        th.start()
+        inside.wait(5)
+    assert sys.getswitchinterval() == pytest.approx(min(prev, 1e-4))  # the other call is still inside
+    go.set()
+    th.join()
+    assert sys.getswitchinterval() == prev

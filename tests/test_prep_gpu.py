@@ -49,3 +49,35 @@ def test_float32_record_keeps_its_dtype(device, case):
     ref = g[case + "_surface_wave_f32"]
     assert got.dtype == np.float32 and got.shape == ref.shape
     assert np.abs(got.astype(np.float64) - ref).max() <= 2e-6 * np.abs(ref).max(), case
+
+
+@pytest.mark.parametrize("n_rows,n_t,dtype,pad", [(640, 28000, np.float64, 0), (256, 140000, np.float32, 24)])
+def test_sosfiltfilt_long_blocks_and_strided_rows(device, n_rows, n_t, dtype, pad):
+    """dvh_sosfiltfilt with blocks longer than 32 samples (the block length grows with the record: L = 96 and 160
+    here, the bench record's 64 in between) and the longer A^L transition; the float32 case on rows of a wider
+    buffer (row stride n_t + 2 pad, the columns outside the rows untouched), through the C ABI.  Against
+    scipy.signal.sosfiltfilt as bandpass_data calls it (oracle/preprocess.py): 1e-10 in float64, 2e-6 in float32."""
+    import torch
+
+    from das_diff_veh_amd import _lib
+    from das_diff_veh_amd.preprocess import _design
+    from oracle import preprocess as oprep
+    dt = 0.004
+    rng = np.random.default_rng(n_t)
+    t = np.arange(n_t) * dt
+    host = (rng.standard_normal((n_rows, n_t)) * 0.1 + np.sin(2 * np.pi * 7.0 * t)[None, :]).astype(dtype)
+    buf = np.full((n_rows, n_t + 2 * pad), 3.5, dtype)
+    buf[:, pad:pad + n_t] = host
+    dev = torch.from_numpy(buf).to(device)
+    rows = dev[:, pad:pad + n_t]
+    sos, padlen, sos_t, zi_t = _design(dt, 1.2, 30, device)
+    nbytes = int(_lib.load().dvh_sosfiltfilt_workspace(n_rows, n_t, len(sos), padlen))
+    work = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+    _lib.call("dvh_sosfiltfilt", _lib.ptr(rows), 0 if dtype == np.float32 else 1, n_rows, rows.stride(0), n_t,
+              _lib.ptr(sos_t), len(sos), padlen, _lib.ptr(zi_t), _lib.ptr(work), _lib.stream_of(device))
+    got = dev.cpu().numpy()
+    ref = oprep.bandpass_data_scipy(host.astype(np.float64), dt, 1.2, 30)
+    tol = 1e-10 if dtype == np.float64 else 2e-6
+    assert np.abs(got[:, pad:pad + n_t].astype(np.float64) - ref).max() <= tol * np.abs(ref).max()
+    if pad:
+        assert np.all(got[:, :pad] == 3.5) and np.all(got[:, pad + n_t:] == 3.5)

@@ -1,6 +1,6 @@
 # SQ counter passes (one rocprofv3 --pmc run each, kernel trace only) over tools/exp_stack.py for one
 # variant of the stack launch; per-dispatch averages -> gpurun_out/pmcx_<tag>.json
-#     bash tools/pmc_exp.sh TAG corr|fused|corr7 [env assignments...]
+#     bash tools/pmc_exp.sh TAG corr|fused|corr7 [env assignments...]   (EXP_ARGS: extra exp_stack.py arguments)
 set -o pipefail
 tag=$1; only=$2; shift 2
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -9,7 +9,7 @@ i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" \
            "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH"; do
   i=$((i+1))
-  env "$@" timeout -s KILL 120 rocprofv3 --pmc $grp -d $d/p$i -o pmc --output-format csv -- python tools/exp_stack.py --reps 3 --only $only > /dev/null 2> $d/p$i.err || { echo "pmc pass $i failed"; tail -3 $d/p$i.err; exit 1; }
+  env "$@" timeout -s KILL 120 rocprofv3 --pmc $grp -d $d/p$i -o pmc --output-format csv -- python tools/exp_stack.py --reps 3 --only $only $EXP_ARGS > /dev/null 2> $d/p$i.err || { echo "pmc pass $i failed"; tail -3 $d/p$i.err; exit 1; }
 done
 python - "$d" << 'PY'
 import csv, glob, json, sys
