@@ -950,6 +950,11 @@ def prep_main(args, world, rank, device):
     bp = float(np.mean([e["bandpass0"].elapsed_time(e["bandpass1"]) for e in evs])) / 1e3
     cl = float(np.mean([e["bandpass1"].elapsed_time(e["cleanup1"]) for e in evs])) / 1e3
     flop = 2.0 * 9 * n_sec * n_ext * n_ch  # sequential sosfiltfilt: forward + backward passes
+    # dvh_sosfiltfilt's block GEMMs on the float64 matrix pipe (csrc/dvh_prep.hip, 32-sample blocks, 16 blocks per
+    # tile): forward end states 2 x 8, forward outputs (lower-triangular Toeplitz + start states) 4 + 8 + 2 x 5,
+    # backward end states 2 x 8, backward outputs 8 + 4 + 2 x 5 v_mfma_f64_16x16x4_f64 per tile (2 NS = 20 states)
+    n_tiles = n_ch * (-(-n_ext // 32)) / 16.0
+    mfma_flop = n_tiles * (16 + 38 + 22) * 2.0 * 16 * 16 * 4
     rec_bytes = 4.0 * n_ch * n_t
     # parity (after timing): the step's output against the reference's own path on the whole record
     # (scipy.signal.sosfiltfilt as bandpass_data calls it, then the imputation and norm), and the bandpass
@@ -976,10 +981,15 @@ def prep_main(args, world, rank, device):
         "trace_samples_per_s": world * args.steps * n_ch * n_t / elapsed,
         "roofline": {"bound": "fp64-valu", "achieved": flop / bp / 1e12, "peak": FP64_VALU_SPEC_TF, "unit": "TFLOP/s",
                      "frac": flop / bp / 1e12 / FP64_VALU_SPEC_TF, "traffic": None,
-                     "kernel": "sos_block_kernel (dvh_sosfiltfilt: transition, 2 x (zero-state blocks, state scan, "
-                               "re-filter))",
+                     "kernel": "dvh_sosfiltfilt (sosm_fa / sosm_scan / sosm_fc / sosm_bf / sosm_scan / sosm_bc: "
+                               "block GEMMs on the float64 MFMA pipe, two-level state scans)",
                      "launch_ms": bp * 1e3, "flop_model": "9 flops per sample per section (scipy sosfilt), forward + "
-                                                          "backward over n_t + 2 padlen; the block form issues 2x",
+                                                          "backward over n_t + 2 padlen (the sequential filter's work)",
+                     "mfma_flop_issued": mfma_flop, "mfma_achieved_tflops": mfma_flop / bp / 1e12,
+                     "mfma_frac_of_spec": mfma_flop / bp / 1e12 / FP64_MFMA_SPEC_TF,
+                     "mfma_model": "32-sample blocks as float64 MFMA GEMMs: 76 v_mfma_f64_16x16x4_f64 per 16 blocks "
+                                   "(forward end states 16, forward outputs + backward end states 38, backward outputs "
+                                   "22), the state scans between them on the VALU",
                      "hbm_bytes_model": "record read + y (f64) written and read + record written",
                      "hbm_frac": (2 * rec_bytes + 16.0 * n_ch * n_ext) / bp / 1e9 / HBM_PEAK_GBS},
         "kernels_ms": {"bandpass": bp * 1e3, "trace_cleanup": cl * 1e3},
@@ -1245,6 +1255,11 @@ def host_main(args, world, rank, device):
         "avg_image_finite": bool(all(np.isfinite(x).all() for x in res_imgs)),
         "cpu_baseline": None,
     }
+    # nothing in flight at exit: the staging side streams and the pinned table uploads are drained (under rocprofv3
+    # the round-4 run ended with 26-30 asynchronous copies still unaccounted for)
+    from das_diff_veh_amd.device import sync_staging
+    sync_staging()
+    torch.cuda.synchronize()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

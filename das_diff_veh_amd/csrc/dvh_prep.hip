@@ -334,6 +334,460 @@ __global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* _
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// sosfiltfilt on the float64 matrix pipe (round 5).  With blocks of kSmL = 32 samples the phases A and C above are
+// GEMMs whose operands are the block's samples and the filter's block operators, all formed on the device from the
+// filter's own recursion (sosm_mats_kernel):
+//   h[t]       the cascade's impulse response (zero state, unit sample at step 0), t < L
+//   Hm[t][m]   its output at step t from the unit state e_m and zero input
+//   g[t][m]    its state after step t from the unit sample at step 0 (zero state)
+//   M = A^L    the zero-input transition of L samples (as sos_transition_kernel), Mzi = M zi
+// A block of L samples u_0..u_{L-1} filtered from start state s gives
+//   outputs   y_i = sum_{j <= i} h[i - j] u_j + sum_m Hm[i][m] s_m            (lower-triangular Toeplitz + L x 2NS)
+//   end state s' = M s + sum_j g[L - 1 - j] u_j                                 (2NS x L)
+// and the backward pass over the reversed forward output, in forward indexing i of the same block (backward
+// blocks aligned with the forward ones; the partial last forward block is the first backward block):
+//   outputs   v_i = sum_{i'' >= i} h[i'' - i] y_i'' + sum_m Hm[L - 1 - i][m] s_m  (upper-triangular Toeplitz)
+//   end state s' = M s + sum_i g[i] y_i
+// The products are v_mfma_f64_16x16x4_f64 tiles over 16 blocks (columns); the state scans between them are
+// sos_scan_kernel's.  Launches:
+//   sosm_fa     forward zero-state end states E_f (block 0 plus M zi x_ext[0]: its true end state)
+//   scan        true forward end states
+//   sosm_fc     forward outputs y from the true start states, written once, and from the same registers the
+//               backward zero-state end states E_b of every full block (the backward phase A, fused)
+//   sosm_bf     the first backward block (the partial last forward block) by the recursion, one lane per row:
+//               its outputs and the backward state after it
+//   scan        true backward end states
+//   sosm_bc     backward outputs from the true start states, trimmed to the row
+// The outputs equal the recursion's up to rounding (sums of <= 52 products per output instead of the cascade's
+// chain); tests/test_prep_gpu.py holds them to scipy.signal.sosfiltfilt at 1e-10 (float64) / 2e-6 (float32).
+constexpr int kSmL = 32;                  // samples per block: two 16-row MFMA tiles
+typedef double doublex4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ doublex4_t mfma_f64x4(double a, double b, doublex4_t c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// offsets (doubles) of the filter operators in the MFMA path's table
+template <int NS>
+struct SosmMats {
+  static constexpr int NST = 2 * NS;
+  static constexpr int h = 0, Hm = kSmL, g = Hm + kSmL * NST, M = g + kSmL * NST, Mzi = M + NST * NST,
+                       MQ = Mzi + NST, size = MQ + NST * NST;
+};
+
+// Experiments e < NST: unit state e_e, zero input (Hm[:, e], M[:, e], and MQ[:, e] = (A^L)^Q e_e after Q L steps,
+// the scan's group transition); e = NST: zero state, unit sample (h, g).
+template <int NS>
+__global__ __launch_bounds__(64) void sosm_mats_kernel(const double* __restrict__ sos, const double* __restrict__ zi,
+                                                       int32_t Q, double* __restrict__ mats) {
+  using O = SosmMats<NS>;
+  constexpr int NST = 2 * NS;
+  const int e = threadIdx.x;
+  SosCoef<NS> c;
+  c.load(sos);
+  if (e <= NST) {
+    double z0[NS], z1[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      z0[s] = (2 * s == e) ? 1.0 : 0.0;
+      z1[s] = (2 * s + 1 == e) ? 1.0 : 0.0;
+    }
+    for (int t = 0; t < kSmL; ++t) {
+      const double o = c.step(z0, z1, (e == NST && t == 0) ? 1.0 : 0.0);
+      if (e == NST) {
+        mats[O::h + t] = o;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          mats[O::g + t * NST + 2 * s] = z0[s];
+          mats[O::g + t * NST + 2 * s + 1] = z1[s];
+        }
+      } else {
+        mats[O::Hm + t * NST + e] = o;
+      }
+    }
+    if (e < NST) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        mats[O::M + (2 * s) * NST + e] = z0[s];
+        mats[O::M + (2 * s + 1) * NST + e] = z1[s];
+      }
+      for (int t = kSmL; t < Q * kSmL; ++t) c.step(z0, z1, 0.0);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        mats[O::MQ + (2 * s) * NST + e] = z0[s];
+        mats[O::MQ + (2 * s + 1) * NST + e] = z1[s];
+      }
+    }
+  }
+  __syncthreads();
+  if (e < NST) {
+    double a = 0.0;
+    for (int j = 0; j < NST; ++j) a += mats[O::M + e * NST + j] * zi[j];
+    mats[O::Mzi + e] = a;
+  }
+}
+
+// sample i of row r of the forward pass's sequence: the odd extension of x (0 past n_ext)
+template <typename T>
+__device__ __forceinline__ double sosm_ext(const T* __restrict__ x, const SosGeom& G, int64_t r, int64_t i) {
+  if (i >= G.n_ext) return 0.0;
+  const T* row = x + r * G.row_stride;
+  const int64_t j = i - G.padlen;
+  if (j >= 0 && j < G.n_t) return (double)row[j];
+  if (j < 0) return 2.0 * (double)row[0] - (double)row[-j];
+  return 2.0 * (double)row[G.n_t - 1] - (double)row[2 * (G.n_t - 1) - j];
+}
+
+// The block operators as MFMA A operands, staged in LDS per block: lane l of k-step kk of row tile t holds
+// A[16 t + (l & 15)][4 kk + (l >> 4)].  op: 0 = G (forward end state, rows = states, k = samples), 1 = T (lower
+// Toeplitz), 2 = U (upper Toeplitz), 3 = Gb (backward end state), 4 = Hm (rows = samples, k = states), 5 = Hm
+// reversed in time.  Zero outside the operator (states >= NST).
+template <int NS>
+__device__ __forceinline__ double sosm_op(const double* __restrict__ mats, int op, int t, int kk, int l) {
+  using O = SosmMats<NS>;
+  constexpr int NST = 2 * NS;
+  const int row = 16 * t + (l & 15), k = 4 * kk + (l >> 4);
+  switch (op) {
+    case 0: return row < NST ? mats[O::g + (kSmL - 1 - k) * NST + row] : 0.0;
+    case 1: return row >= k ? mats[O::h + row - k] : 0.0;
+    case 2: return k >= row ? mats[O::h + k - row] : 0.0;
+    case 3: return row < NST ? mats[O::g + k * NST + row] : 0.0;
+    case 4: return k < NST ? mats[O::Hm + row * NST + k] : 0.0;
+    default: return k < NST ? mats[O::Hm + (kSmL - 1 - row) * NST + k] : 0.0;
+  }
+}
+
+// the 16-column tile's column of this lane: global block g = r nb + k
+struct SosmCol {
+  int64_t g, r;
+  int k;
+  bool valid;
+};
+__device__ __forceinline__ SosmCol sosm_col(const SosGeom& G, int64_t tile, int lane) {
+  SosmCol c;
+  c.g = tile * 16 + (lane & 15);
+  c.valid = c.g < G.n_rows * G.nb;
+  c.r = c.valid ? c.g / G.nb : 0;
+  c.k = c.valid ? (int)(c.g - c.r * G.nb) : 0;
+  return c;
+}
+
+// Forward phase A: E_f[g] = G u_block for k < nb - 1 (block 0: + M zi u_0, its true end state).
+template <typename T, int NS>
+__global__ __launch_bounds__(256) void sosm_fa_kernel(const T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
+                                                      double* __restrict__ Sf) {
+  using O = SosmMats<NS>;
+  constexpr int NST = 2 * NS, RT = (NST + 15) / 16;
+  __shared__ double opA[RT][8][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int q = threadIdx.x; q < RT * 8 * 64; q += 256) opA[q / 512][(q / 64) % 8][q % 64] = sosm_op<NS>(mats, 0, q / 512, (q / 64) % 8, q % 64);
+  __syncthreads();
+  const int64_t n_tiles = (G.n_rows * G.nb + 15) / 16;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    const SosmCol c = sosm_col(G, tile, lane);
+    const bool full = c.valid && c.k < G.nb - 1;
+    double b[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) b[kk] = full ? sosm_ext(x, G, c.r, (int64_t)c.k * kSmL + 4 * kk + (lane >> 4)) : 0.0;
+    doublex4_t acc[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) acc[t] = mfma_f64x4(opA[t][kk][lane], b[kk], acc[t]);
+    }
+    const double u0 = (full && c.k == 0) ? sosm_ext(x, G, c.r, 0) : 0.0;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int m = 16 * t + 4 * rr + (lane >> 4);
+        if (full && m < NST) Sf[c.g * NST + m] = acc[t][rr] + u0 * mats[O::Mzi + m];
+      }
+  }
+}
+
+// Forward phase C + backward phase A: y = T u + Hm s (s: the true start state, zi u_0 for block 0), then
+// E_b = Gb y from the same registers, stored at the backward block index nb - 1 - k (full blocks only).
+template <typename T, int NS>
+__global__ __launch_bounds__(256) void sosm_fc_kernel(const T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
+                                                      const double* __restrict__ zi, const double* __restrict__ Sf,
+                                                      double* __restrict__ y, double* __restrict__ Sb) {
+  constexpr int NST = 2 * NS, RT = (NST + 15) / 16, KS = (NST + 3) / 4;
+  __shared__ double opT[2][8][64], opH[2][KS][64], opG[RT][8][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int q = threadIdx.x; q < 2 * 8 * 64; q += 256) opT[q / 512][(q / 64) % 8][q % 64] = sosm_op<NS>(mats, 1, q / 512, (q / 64) % 8, q % 64);
+  for (int q = threadIdx.x; q < 2 * KS * 64; q += 256)
+    opH[q / (KS * 64)][(q / 64) % KS][q % 64] = sosm_op<NS>(mats, 4, q / (KS * 64), (q / 64) % KS, q % 64);
+  for (int q = threadIdx.x; q < RT * 8 * 64; q += 256) opG[q / 512][(q / 64) % 8][q % 64] = sosm_op<NS>(mats, 3, q / 512, (q / 64) % 8, q % 64);
+  __syncthreads();
+  const int64_t n_tiles = (G.n_rows * G.nb + 15) / 16;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    const SosmCol c = sosm_col(G, tile, lane);
+    const int64_t i0 = (int64_t)c.k * kSmL;
+    double b[8], sv[KS];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) b[kk] = c.valid ? sosm_ext(x, G, c.r, i0 + 4 * kk + (lane >> 4)) : 0.0;
+    const double u0 = (c.valid && c.k == 0) ? sosm_ext(x, G, c.r, 0) : 0.0;
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+      const int m = 4 * q + (lane >> 4);
+      sv[q] = (!c.valid || m >= NST) ? 0.0 : (c.k == 0 ? zi[m] * u0 : Sf[(c.g - 1) * NST + m]);
+    }
+    doublex4_t acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 4 * (t + 1); ++kk) acc[t] = mfma_f64x4(opT[t][kk][lane], b[kk], acc[t]);  // lower triangle
+#pragma unroll
+      for (int q = 0; q < KS; ++q) acc[t] = mfma_f64x4(opH[t][q][lane], sv[q], acc[t]);
+    }
+    const int64_t P = c.k == G.nb - 1 ? G.n_ext - i0 : kSmL;
+    double* yr = y + c.r * G.n_ext + i0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int i = 16 * t + 4 * rr + (lane >> 4);
+        if (c.valid && i < P) yr[i] = acc[t][rr];
+      }
+    // backward zero-state end state of this block: Gb y, y (rows = samples) as the B operand straight from the
+    // accumulators (D register rr of tile t is k-step 4 t + rr)
+    doublex4_t e[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      e[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) e[t] = mfma_f64x4(opG[t][kk][lane], acc[kk >> 2][kk & 3], e[t]);
+    }
+    const bool fullb = c.valid && c.k < G.nb - 1;
+    double* sb = Sb + (c.r * G.nb + (G.nb - 1 - c.k)) * NST;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int m = 16 * t + 4 * rr + (lane >> 4);
+        if (fullb && m < NST) sb[m] = e[t][rr];
+      }
+  }
+}
+
+// The first backward block (forward block nb - 1, P = n_ext - (nb - 1) L samples) by the recursion from zi y[-1],
+// one lane per row: its outputs (trimmed) and the backward state after it (Sb[r][0]).
+template <typename T, int NS>
+__global__ __launch_bounds__(64) void sosm_bf_kernel(T* __restrict__ x, SosGeom G, const double* __restrict__ sos,
+                                                     const double* __restrict__ zi, const double* __restrict__ y,
+                                                     double* __restrict__ Sb) {
+  constexpr int NST = 2 * NS;
+  const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (r >= G.n_rows) return;
+  SosCoef<NS> c;
+  c.load(sos);
+  const double* yr = y + r * G.n_ext;
+  const double ul = yr[G.n_ext - 1];
+  double z0[NS], z1[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    z0[q] = zi[2 * q] * ul;
+    z1[q] = zi[2 * q + 1] * ul;
+  }
+  const int64_t start = (int64_t)(G.nb - 1) * kSmL;
+  for (int64_t i = G.n_ext - 1; i >= start; --i) {
+    const double v = c.step(z0, z1, yr[i]);
+    const int64_t j = i - G.padlen;
+    if (j >= 0 && j < G.n_t) x[r * G.row_stride + j] = (T)v;
+  }
+  double* sb = Sb + r * G.nb * NST;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    sb[2 * q] = z0[q];
+    sb[2 * q + 1] = z1[q];
+  }
+}
+
+// Backward phase C for backward blocks k' >= 1 (forward blocks k = nb - 1 - k' < nb - 1): v = U y + Hrev s with s
+// the true backward state before the block, written into the row (trimmed).
+template <typename T, int NS>
+__global__ __launch_bounds__(256) void sosm_bc_kernel(T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
+                                                      const double* __restrict__ y, const double* __restrict__ Sb) {
+  constexpr int NST = 2 * NS, KS = (NST + 3) / 4;
+  __shared__ double opU[2][8][64], opH[2][KS][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int q = threadIdx.x; q < 2 * 8 * 64; q += 256) opU[q / 512][(q / 64) % 8][q % 64] = sosm_op<NS>(mats, 2, q / 512, (q / 64) % 8, q % 64);
+  for (int q = threadIdx.x; q < 2 * KS * 64; q += 256)
+    opH[q / (KS * 64)][(q / 64) % KS][q % 64] = sosm_op<NS>(mats, 5, q / (KS * 64), (q / 64) % KS, q % 64);
+  __syncthreads();
+  // columns: (r, k) with k < nb - 1, i.e. nb - 1 per row
+  const int nbc = G.nb - 1;
+  const int64_t n_cols = G.n_rows * nbc, n_tiles = (n_cols + 15) / 16;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t g = tile * 16 + (lane & 15);
+    const bool valid = g < n_cols;
+    const int64_t r = valid ? g / nbc : 0;
+    const int k = valid ? (int)(g - r * nbc) : 0;
+    const double* yr = y + r * G.n_ext + (int64_t)k * kSmL;
+    double b[8], sv[KS];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) b[kk] = valid ? yr[4 * kk + (lane >> 4)] : 0.0;
+    const double* sb = Sb + (r * G.nb + (G.nb - 2 - k)) * NST;  // backward block k' - 1 = nb - 2 - k
+#pragma unroll
+    for (int q = 0; q < KS; ++q) {
+      const int m = 4 * q + (lane >> 4);
+      sv[q] = (valid && m < NST) ? sb[m] : 0.0;
+    }
+    doublex4_t acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 4 * t; kk < 8; ++kk) acc[t] = mfma_f64x4(opU[t][kk][lane], b[kk], acc[t]);  // upper triangle
+#pragma unroll
+      for (int q = 0; q < KS; ++q) acc[t] = mfma_f64x4(opH[t][q][lane], sv[q], acc[t]);
+    }
+    T* xr = x + r * G.row_stride;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int64_t j = (int64_t)k * kSmL + 16 * t + 4 * rr + (lane >> 4) - G.padlen;
+        if (valid && j >= 0 && j < G.n_t) xr[j] = (T)acc[t][rr];
+      }
+  }
+}
+
+// The state scan S[k] = S[k] + M S[k - 1], k = 1 .. K - 1 (K = nb - 1 end states; S[0] already true; S[k] holds
+// the zero-state end state E[k] on entry), two-level: one 512-thread block per row, 16 half-waves (lane j = state
+// component j).  The steps are cut into NG <= 16 groups of Q (q covers k in [1 + q Q, 1 + (q + 1) Q)):
+//   1  every group runs the scan from a zero start (group 0 from S[0]): Z[k] = E[k] + M Z[k - 1] (into S[k]);
+//   2  the carries, in order: C_q = Z[last of q] + M^Q C_{q - 1} (C_0 = Z[last of 0], already true);
+//   3  every group q >= 1 adds the carried part: D = M D from D = C_{q - 1}, S[k] = Z[k] + D.
+// 2 Q + NG dependent steps instead of K - 1 (record of 1 024 x 60 s: 76 instead of 471).  M^Q is formed by the
+// recursion (sosm_mats_kernel).
+constexpr int kScanHW = 16;
+__host__ __device__ constexpr int sosm_scan_q(int nb) { return nb > 2 ? (nb - 2 + kScanHW - 1) / kScanHW : 1; }
+
+template <int NS>
+__global__ __launch_bounds__(512) void sosm_scan_kernel(SosGeom G, const double* __restrict__ mats, int32_t Q,
+                                                        double* __restrict__ S) {
+  using O = SosmMats<NS>;
+  constexpr int NST = 2 * NS;
+  __shared__ __attribute__((aligned(16))) double sv[kScanHW][32];
+  __shared__ double carry[kScanHW][NST];
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const bool act = j < NST;
+  const int64_t r = blockIdx.x;
+  double* Sr = S + r * (int64_t)G.nb * NST;
+  const int K = G.nb - 1;
+  const int k0 = 1 + hw * Q, k1 = min(1 + (hw + 1) * Q, K);  // this half-wave's group [k0, k1)
+  // one matvec step: out_j = add + sum_i A[j][i] x_i, x from this half-wave's LDS slot (every lane of the wave runs
+  // the same steps; lanes of an empty group compute on zeros)
+  double m[NST];
+#pragma unroll
+  for (int i = 0; i < NST; ++i) m[i] = act ? mats[O::M + j * NST + i] : 0.0;
+  auto matvec = [&](const double (&A)[NST], double add) {
+    wave_barrier_lds();
+    const double2* v2 = reinterpret_cast<const double2*>(sv[hw]);
+    double pa[4] = {add, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < NST / 2; ++i) {
+      const double2 u = v2[i];
+      pa[(2 * i) & 3] += A[2 * i] * u.x;
+      pa[(2 * i + 1) & 3] += A[2 * i + 1] * u.y;
+    }
+    return (pa[0] + pa[1]) + (pa[2] + pa[3]);
+  };
+  // level 1: zero-start scans of the groups (group 0 from the true S[0])
+  double z = (hw == 0 && act) ? Sr[j] : 0.0;
+  sv[hw][j] = z;
+  const int nmax = Q;  // every half-wave runs Q steps; those past its group compute on zeros and store nothing
+  double e = (act && k0 < k1) ? Sr[(int64_t)k0 * NST + j] : 0.0;
+  for (int t = 0; t < nmax; ++t) {
+    const int k = k0 + t;
+    const double en = (act && k + 1 < k1) ? Sr[(int64_t)(k + 1) * NST + j] : 0.0;  // the next E under this step
+    z = matvec(m, e);
+    if (act && k < k1) Sr[(int64_t)k * NST + j] = z;
+    wave_barrier_lds();
+    sv[hw][j] = z;
+    e = en;
+  }
+  // the group's last Z is in sv[hw] (steps past the group keep z = M^t Z_last + 0: they do not, so keep it apart)
+  __syncthreads();
+  const int ng = K > 1 ? (K - 1 + Q - 1) / Q : 0;  // non-empty groups
+  // level 2: carries by one half-wave
+  if (hw == 0) {
+    double mq[NST];
+#pragma unroll
+    for (int i = 0; i < NST; ++i) mq[i] = act ? mats[O::MQ + j * NST + i] : 0.0;
+    double c = (act && ng > 0) ? Sr[(int64_t)(min(1 + Q, K) - 1) * NST + j] : 0.0;  // C_0 = S[last of group 0]
+    if (act) carry[0][j] = c;
+    for (int q = 1; q + 1 < ng; ++q) {
+      wave_barrier_lds();
+      sv[0][j] = c;
+      const double zl = act ? Sr[(int64_t)(min(1 + (q + 1) * Q, K) - 1) * NST + j] : 0.0;
+      c = matvec(mq, zl);
+      if (act) carry[q][j] = c;
+    }
+  }
+  __syncthreads();
+  // level 3: the carried part of groups q >= 1
+  if (hw >= 1 && hw < ng) {
+    double d = act ? carry[hw - 1][j] : 0.0;
+    for (int k = k0; k < k1; ++k) {
+      wave_barrier_lds();
+      sv[hw][j] = d;
+      d = matvec(m, 0.0);
+      if (act) Sr[(int64_t)k * NST + j] += d;
+    }
+  }
+}
+
+static SosGeom sosm_geom(int64_t n_rows, int64_t row_stride, int32_t n_t, int32_t padlen) {
+  SosGeom G;
+  G.n_rows = n_rows;
+  G.row_stride = row_stride;
+  G.n_t = n_t;
+  G.padlen = padlen;
+  G.n_ext = (int64_t)n_t + 2 * padlen;
+  G.L = kSmL;
+  G.nb = (int32_t)((G.n_ext + kSmL - 1) / kSmL);
+  return G;
+}
+
+// workspace of the MFMA path: y [n_rows][n_ext] + Sf, Sb [n_rows][nb][2 n_sec] + the operator table, doubles
+static int64_t sosm_workspace_doubles(const SosGeom& G, int n_sec) {
+  const int64_t nst = 2 * n_sec;
+  return G.n_rows * G.n_ext + 2 * G.n_rows * G.nb * nst + (kSmL + 2 * kSmL * nst + 2 * nst * nst + nst);
+}
+
+template <typename T, int NS>
+static int sosfiltfilt_mfma(T* x, const SosGeom& G, const double* sos, const double* zi, double* work, hipStream_t st) {
+  constexpr int NST = 2 * NS;
+  double* y = work;
+  double* Sf = y + G.n_rows * G.n_ext;
+  double* Sb = Sf + G.n_rows * G.nb * NST;
+  double* mats = Sb + G.n_rows * G.nb * NST;
+  const int64_t tiles = (G.n_rows * G.nb + 15) / 16;
+  const unsigned grid = (unsigned)std::min<int64_t>((tiles + 3) / 4, 65535);
+  const int Q = sosm_scan_q(G.nb);
+  hipLaunchKernelGGL(sosm_mats_kernel<NS>, dim3(1), dim3(64), 0, st, sos, zi, Q, mats);
+  if (G.nb > 1) hipLaunchKernelGGL((sosm_fa_kernel<T, NS>), dim3(grid), dim3(256), 0, st, (const T*)x, G, (const double*)mats, Sf);
+  if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, (const double*)mats, Q, Sf);
+  hipLaunchKernelGGL((sosm_fc_kernel<T, NS>), dim3(grid), dim3(256), 0, st, (const T*)x, G, (const double*)mats, zi,
+                     (const double*)Sf, y, Sb);
+  hipLaunchKernelGGL((sosm_bf_kernel<T, NS>), dim3((unsigned)((G.n_rows + 63) / 64)), dim3(64), 0, st, x, G, sos, zi,
+                     (const double*)y, Sb);
+  if (G.nb > 1) {
+    if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, (const double*)mats, Q, Sb);
+    const int64_t tb = (G.n_rows * (G.nb - 1) + 15) / 16;
+    hipLaunchKernelGGL((sosm_bc_kernel<T, NS>), dim3((unsigned)std::min<int64_t>((tb + 3) / 4, 65535)), dim3(256), 0, st, x, G,
+                       (const double*)mats, (const double*)y, (const double*)Sb);
+  }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
+}
+
 // block length: enough (row, block) lanes for ~4 waves per SIMD, blocks of 32 .. 4096 samples
 static int sos_block_len(int64_t n_rows, int64_t n_ext) {
   const int64_t target = 256LL * 4 * 4 * 64;
@@ -382,12 +836,16 @@ static int sosfiltfilt_blocks(T* x, const SosGeom& G, const double* sos, const d
   return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
 }
 
+#ifndef DVH_SOS_MFMA
+#define DVH_SOS_MFMA 1  // sosfiltfilt's block phases as float64 MFMA GEMMs (0: the VALU recursion per (row, block) lane)
+#endif
+
 template <typename T>
 static int sosfiltfilt_dispatch(T* x, const SosGeom& G, const double* sos, int n_sec, const double* zi, double* work,
                                 hipStream_t st) {
   switch (n_sec) {
 #define DVH_SOS_CASE(n) \
-  case n: return sosfiltfilt_blocks<T, n>(x, G, sos, zi, work, st);
+  case n: return DVH_SOS_MFMA ? sosfiltfilt_mfma<T, n>(x, G, sos, zi, work, st) : sosfiltfilt_blocks<T, n>(x, G, sos, zi, work, st);
     DVH_SOS_CASE(1) DVH_SOS_CASE(2) DVH_SOS_CASE(3) DVH_SOS_CASE(4) DVH_SOS_CASE(5) DVH_SOS_CASE(6)
     DVH_SOS_CASE(7) DVH_SOS_CASE(8) DVH_SOS_CASE(9) DVH_SOS_CASE(10) DVH_SOS_CASE(11) DVH_SOS_CASE(12)
     DVH_SOS_CASE(13) DVH_SOS_CASE(14) DVH_SOS_CASE(15) DVH_SOS_CASE(16)
@@ -586,7 +1044,8 @@ DVH_API int dvh_trace_cleanup(void* x, int32_t dtype, int64_t n_rows, int64_t ro
 
 DVH_API int64_t dvh_sosfiltfilt_workspace(int64_t n_rows, int32_t n_t, int32_t n_sec, int32_t padlen) {
   if (n_rows <= 0 || n_t <= 0 || n_sec <= 0 || n_sec > kMaxSec || padlen < 0) return 0;
-  return 8 * sos_workspace_doubles(sos_geom(n_rows, n_t, n_t, padlen), n_sec);
+  return 8 * (DVH_SOS_MFMA ? sosm_workspace_doubles(sosm_geom(n_rows, n_t, n_t, padlen), n_sec)
+                           : sos_workspace_doubles(sos_geom(n_rows, n_t, n_t, padlen), n_sec));
 }
 
 DVH_API int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t,
@@ -597,7 +1056,7 @@ DVH_API int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_
   if (n_t <= padlen) return set_error(-4, "The length of the input vector x must be greater than padlen");
   if (padlen < 0 || n_t < 2) return set_error(-2, "invalid padlen / length");
   if (n_rows <= 0) return 0;
-  const SosGeom G = sos_geom(n_rows, row_stride, n_t, padlen);
+  const SosGeom G = DVH_SOS_MFMA ? sosm_geom(n_rows, row_stride, n_t, padlen) : sos_geom(n_rows, row_stride, n_t, padlen);
   if (dtype == 0) return sosfiltfilt_dispatch<float>((float*)x, G, sos, n_sec, zi, work, (hipStream_t)stream);
   if (dtype == 1) return sosfiltfilt_dispatch<double>((double*)x, G, sos, n_sec, zi, work, (hipStream_t)stream);
   return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");

@@ -1270,6 +1270,9 @@ static int cu_count() {
 #ifndef DVH_VSTACK_BPC
 #define DVH_VSTACK_BPC 2  // blocks per CU
 #endif
+#ifndef DVH_VSTACK_OCC
+#define DVH_VSTACK_OCC 4  // EngF500 validated launch: waves per SIMD the registers are sized for (launch bounds)
+#endif
 #ifndef DVH_PIVOT_TABLE
 #define DVH_PIVOT_TABLE 1  // stack launches at w = 500 with the per-pass pivot-slice spectra table
 #endif
@@ -1287,7 +1290,7 @@ static VStack vstack(int bpc) {
 }
 static bool get_vstack(int n, VStack* v) {
   switch (n) {
-    case 500: *v = vstack<EngF500, DVH_VSTACK_FFT, DVH_VSTACK_SCAN, 4, true>(DVH_VSTACK_BPC); return true;
+    case 500: *v = vstack<EngF500, DVH_VSTACK_FFT, DVH_VSTACK_SCAN, DVH_VSTACK_OCC, true>(DVH_VSTACK_BPC); return true;
     case 512: *v = vstack<EngStockham<512, true>, 7, 1, 2, false>(1); return true;
     case 1024: *v = vstack<EngP1024, 7, 1, 2, false>(1); return true;
     default: return false;

@@ -163,23 +163,45 @@ template <> struct Dft<5> {
   }
 };
 
-template <int N, int Ls, int R>
+// Swizzled LDS layout (SW = 1, the padded 1 024-point engine): element n lives at n ^ (((n >> 4) & 3) << 2), i.e.
+// bits 4-5 of the index are XORed into bits 2-3.  Radix-4 stages write out[(i - k) R + k + q Ls]: at Ls = 4 a
+// 16-lane store group (ds_write_b64, 32 banks = 16 complex slots) spans four 128-byte rows at the same bank offset
+// (a 4-way conflict in the plain layout); the swizzle spreads the four rows over distinct bank quarters.  Contiguous
+// reads stay conflict-free (the map permutes bits 0-4 within every aligned run of 32), and bits >= 6 are untouched,
+// so offsets that are multiples of 64 commute with it.
+template <int SW>
+__device__ __forceinline__ int lds_idx(int n) {
+  return SW ? (n ^ (((n >> 4) & 3) << 2)) : n;
+}
+// With SW, the stage twiddles w1 = tw[k (N / (Ls R))] of the stages with 4 <= Ls and a table stride > 1 are also
+// held contiguously in k after the main table (tw[N + (Ls - 4) / 3 + k], Ls = 4, 16, 64, N <= 1024;
+// tw_entries<N, 1>): a strided read of the main table puts up to 16 distinct addresses of a lane group on one or
+// two banks.
+template <int N, int SW>
+constexpr int tw_entries() {
+  return SW ? N + (N > 16 ? 4 : 0) + (N > 64 ? 16 : 0) + (N > 256 ? 64 : 0) : N;  // stages Ls < N / 4
+}
+
+template <int N, int Ls, int R, int SW = 0>
 __device__ __forceinline__ void stockham_stage(const float2* __restrict__ in, float2* __restrict__ out,
                                                const float2* __restrict__ tw, int lane) {
   constexpr int NB = N / R;
   constexpr int TWS = N / (Ls * R);
   static_assert(N % (Ls * R) == 0, "plan does not divide N");
+  static_assert(!SW || (R == 4 && NB % 64 == 0 && N <= 1024 && (TWS == 1 || Ls == 4 || Ls == 16 || Ls == 64)),
+                "the swizzled layout is for power-of-4 stages whose reads are 64-aligned runs");
   auto round = [&](int i0) {
     const int i = i0 + lane;
     if (NB % 64 == 0 || i < NB) {
       const int k = i % Ls;
       float2 a[R];
+      const int ib = lds_idx<SW>(i);  // + t NB: NB is a multiple of 64 when SW
 #pragma unroll
-      for (int t = 0; t < R; ++t) a[t] = lds_ld(in, i + t * NB);
+      for (int t = 0; t < R; ++t) a[t] = lds_ld(in, ib + t * NB);
       if (Ls > 1) {
 #if DVH_TW_RECUR
         // one table read per butterfly, powers by recurrence (LDS reads are the scarcer resource)
-        const float2 w1 = tw[k * TWS];
+        const float2 w1 = (SW && TWS > 1) ? tw[N + (Ls - 4) / 3 + k] : tw[k * TWS];
         float2 wt = w1;
 #pragma unroll
         for (int t = 1; t < R; ++t) {
@@ -194,7 +216,7 @@ __device__ __forceinline__ void stockham_stage(const float2* __restrict__ in, fl
       Dft<R>::run(a);
       const int base = (i - k) * R + k;
 #pragma unroll
-      for (int q = 0; q < R; ++q) out[base + q * Ls] = a[q];
+      for (int q = 0; q < R; ++q) out[lds_idx<SW>(base + q * Ls)] = a[q];
     }
   };
   // Short radix <= 5 stages (<= 2 rounds of 64 butterflies) are unrolled so that the second round's LDS reads
@@ -234,13 +256,19 @@ template <> struct FftPlan<512> { using T = Stockham<512, 1, 4, 4, 4, 4, 2>; };
 template <> struct FftPlan<1024> { using T = Stockham<1024, 1, 4, 4, 4, 4, 4>; };
 template <> struct FftPlan<2048> { using T = Stockham<2048, 1, 4, 4, 4, 4, 4, 2>; };
 
-// Block-cooperative twiddle table tw[m] = exp(-2*pi*i*m/N), computed in double then rounded.
-template <int N>
+// Block-cooperative twiddle table tw[m] = exp(-2*pi*i*m/N), computed in double then rounded; with SW also the
+// contiguous stage tables of stockham_stage<..., SW = 1> (the same values: entry (Ls, k) is tw[k N / (4 Ls)]).
+template <int N, int SW = 0>
 __device__ __forceinline__ void init_twiddles(float2* tw) {
-  for (int m = threadIdx.x; m < N; m += blockDim.x) {
+  for (int e = threadIdx.x; e < tw_entries<N, SW>(); e += blockDim.x) {
+    int m = e;
+    if (e >= N) {  // stage table entry: Ls = 4, 16, 64 at offsets 0, 4, 20
+      const int o = e - N, Ls = o < 4 ? 4 : (o < 20 ? 16 : 64), k = o - (Ls - 4) / 3;
+      m = k * (N / (4 * Ls));
+    }
     double s, c;
     sincospi(2.0 * (double)m / (double)N, &s, &c);
-    tw[m] = make_float2((float)c, (float)(-s));
+    tw[e] = make_float2((float)c, (float)(-s));
   }
 }
 

@@ -855,11 +855,14 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   static constexpr int kWaves = 4;
   static constexpr bool kNextTask = false;
   static constexpr int kTabBins = 520;  // bins f <= 512; [519].x: the slice's non-zero flag
-  static constexpr size_t kBlockBytes = sizeof(float2) * N;     // twiddle table
-  static constexpr size_t kWaveBytes = sizeof(float2) * 2 * N;  // ping-pong buffers
+  // LDS layout: the swizzled one of stockham_stage<..., SW = 1> (lds_idx<1>) in both buffers, and the twiddle table
+  // with its contiguous stage tables (conflict-free twiddle reads and stage stores: the round-4 build spent 2.9 bank-
+  // conflict cycles per LDS instruction, the Ls = 4 stores and the strided twiddle reads)
+  static constexpr size_t kBlockBytes = sizeof(float2) * tw_entries<N, 1>();  // twiddle tables
+  static constexpr size_t kWaveBytes = sizeof(float2) * 2 * N;                // ping-pong buffers
 
   __device__ EngP1024(char* lds, int wave, int lane_) : FusedOps<EngP1024, 8, 9>(lds, wave, lane_, N / 2) {}
-  static __device__ void block_init(char* lds) { init_twiddles<N>(reinterpret_cast<float2*>(lds)); }
+  static __device__ void block_init(char* lds) { init_twiddles<N, 1>(reinterpret_cast<float2*>(lds)); }
 
   static __device__ __forceinline__ int bin(int l, int j) {
     switch (j) {
@@ -887,27 +890,33 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
     }
   }
 
+  // the four outputs of radix-4 butterfly i of a span-1 stage (out[4 i + q] in the swizzled layout, whose 4-element
+  // groups stay contiguous: lds_idx<1>(4 i + q) = 4 (i ^ ((i >> 2) & 3)) + q) as two 16-byte stores at a 32-byte
+  // lane stride; lanes with i & 4 store their second pair first so that every 8-lane store group tiles the 32 banks
+  // (as EngF500's stage 1)
+  static __device__ __forceinline__ void store4(float2* out, int i, float2 x0, float2 x1, float2 x2, float2 x3) {
+    const bool sw = (i & 4) != 0;
+    const int o = sw ? 2 : 0;
+    float4* d = reinterpret_cast<float4*>(out + lds_idx<1>(4 * i));
+    d[o >> 1] = sw ? make_float4(x2.x, x2.y, x3.x, x3.y) : make_float4(x0.x, x0.y, x1.x, x1.y);
+    d[(2 - o) >> 1] = sw ? make_float4(x0.x, x0.y, x1.x, x1.y) : make_float4(x2.x, x2.y, x3.x, x3.y);
+  }
+
   __device__ __forceinline__ void stage1(const float2 (&z)[8]) const {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = lane + 64 * r;
       const float2 a0 = z[r], a1 = z[r + 4];
       // radix-4 DFT of (a0, a1, 0, 0)
-      const float2 x0 = cadd(a0, a1), x1 = add_mi(a0, a1), x2 = csub(a0, a1), x3 = add_pi(a0, a1);
-      // two 16-byte stores at a 32-byte lane stride; lanes with i & 4 store their second pair first so that
-      // every 8-lane store group tiles the 32 banks (as EngF500's stage 1)
-      const bool sw = (lane & 4) != 0;
-      const int o = sw ? 2 : 0;
-      float4* d = reinterpret_cast<float4*>(bufB + 4 * i);
-      d[o >> 1] = sw ? make_float4(x2.x, x2.y, x3.x, x3.y) : make_float4(x0.x, x0.y, x1.x, x1.y);
-      d[(2 - o) >> 1] = sw ? make_float4(x0.x, x0.y, x1.x, x1.y) : make_float4(x2.x, x2.y, x3.x, x3.y);
+      store4(bufB, i, cadd(a0, a1), add_mi(a0, a1), csub(a0, a1), add_pi(a0, a1));
     }
   }
 
   // radix-4 butterfly k of the last stage (span 256): X[k + 256 q], q < 4
   __device__ __forceinline__ void last_bfly_from(const float2* src, int k, float2 (&x)[4]) const {
+    const int kb = lds_idx<1>(k);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) x[t] = lds_ld(src, k + 256 * t);
+    for (int t = 0; t < 4; ++t) x[t] = lds_ld(src, kb + 256 * t);
     const float2 w1 = tw[k];
     float2 wt = w1;
 #pragma unroll
@@ -927,11 +936,11 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   template <class F>
   __device__ __forceinline__ void finish_with(F&& acc) const {
     wave_sync();
-    stockham_stage<N, 4, 4>(bufB, bufA, tw, lane);
+    stockham_stage<N, 4, 4, 1>(bufB, bufA, tw, lane);
     wave_sync();
-    stockham_stage<N, 16, 4>(bufA, bufB, tw, lane);
+    stockham_stage<N, 16, 4, 1>(bufA, bufB, tw, lane);
     wave_sync();
-    stockham_stage<N, 64, 4>(bufB, bufA, tw, lane);
+    stockham_stage<N, 64, 4, 1>(bufB, bufA, tw, lane);
     wave_sync();
     const int ln = opaque(lane);  // the stage's addresses formed per call, not held in registers between calls
     const bool l0 = ln == 0;
@@ -957,10 +966,39 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
     wave_sync();
   }
 
+  // The inverse transform conj(FFT(conj(W))) of W = Cf + i Co (W[N - f] = conj Cf[f] + i conj Co[f]).  Its first
+  // stage (span 1: butterfly i of x[i + 256 t], t < 4, no twiddles) runs from the registers: the inputs of each
+  // butterfly are four of ONE lane's half-spectrum slots or their Hermitian partners -- lane l >= 1 holds those of
+  // butterflies l, 64 + l, 192 - l and 256 - l, lane 0 those of 0, 64, 128 and 192 -- so the spectrum is never
+  // stored and re-read; then stages 2-5 in the swizzled layout.  Returns Y (bufB), read through c().
   __device__ const float2* inverse(const float2 (&Cf)[NH], const float2 (&Co)[NH]) {
-    store_conj_hermitian<EngP1024>(bufA, Cf, Co, lane);
+    const int ln = opaque(lane);
+    const bool l0 = ln == 0;
+    // x[f] = conj W[f] = A(j), x[N - f] = conj W[N - f] = B(j) for slot j's bin f
+    auto A = [&](int j) { return make_float2(Cf[j].x - Co[j].y, -(Cf[j].y + Co[j].x)); };
+    auto B = [&](int j) { return make_float2(Cf[j].x + Co[j].y, Cf[j].y - Co[j].x); };
+    auto bfly = [&](int i, float2 a0, float2 a1, float2 a2, float2 a3) {
+      float2 a[4] = {a0, a1, a2, a3};
+      Dft<4>::run(a);
+      store4(bufB, i, a[0], a[1], a[2], a[3]);
+    };
+    // lane 0: x[512] is bin 512 itself (slot 8), x[768] the partner of bin 256 (slot 1); lanes >= 1: partners of
+    // 512 - l (slot 3) and 256 - l (slot 2)
+    bfly(ln, A(0), A(1), l0 ? A(8) : B(3), l0 ? B(1) : B(2));
+    bfly(64 + ln, A(4), A(5), B(7), B(6));
+    // lanes >= 1: butterflies 192 - l and 256 - l; lane 0: 128 and 192 (value selects, no divergent branch)
+    bfly(l0 ? 128 : 192 - ln, sel(l0, A(2), A(6)), sel(l0, A(3), A(7)), sel(l0, B(3), B(5)), sel(l0, B(2), B(4)));
+    bfly(l0 ? 192 : 256 - ln, sel(l0, A(6), A(2)), sel(l0, A(7), A(3)), sel(l0, B(5), B(1)), sel(l0, B(4), B(0)));
     wave_sync();
-    return FftPlan<N>::T::run(bufA, bufB, tw, lane);
+    stockham_stage<N, 4, 4, 1>(bufB, bufA, tw, lane);
+    wave_sync();
+    stockham_stage<N, 16, 4, 1>(bufA, bufB, tw, lane);
+    wave_sync();
+    stockham_stage<N, 64, 4, 1>(bufB, bufA, tw, lane);
+    wave_sync();
+    stockham_stage<N, 256, 4, 1>(bufA, bufB, tw, lane);
+    wave_sync();
+    return bufB;
   }
 
   __device__ const float2* correlate(const RowTask& t, const RowTask& nt, bool has_next, int w_, int hop) {
@@ -973,9 +1011,9 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
 
   // (N * sum_s c_f[k], N * sum_s c_o[k]): the linear correlation folded to the circular one of period w
   __device__ float2 c(const float2* Y, int k, int w_) const {
-    float2 v = Y[k];
+    float2 v = Y[lds_idx<1>(k)];
     if (k > 0) {
-      const float2 u = Y[N - w_ + k];
+      const float2 u = Y[lds_idx<1>(N - w_ + k)];
       v.x += u.x;
       v.y += u.y;
     }
