@@ -837,7 +837,7 @@ static int sosfiltfilt_blocks(T* x, const SosGeom& G, const double* sos, const d
 }
 
 #ifndef DVH_SOS_MFMA
-#define DVH_SOS_MFMA 1  // sosfiltfilt's block phases as float64 MFMA GEMMs (0: the VALU recursion per (row, block) lane)
+#define DVH_SOS_MFMA 0  // sosfiltfilt's block phases as float64 MFMA GEMMs (0: the VALU recursion per (row, block) lane)
 #endif
 
 template <typename T>

@@ -169,11 +169,12 @@ template <> struct Dft<5> {
 // (a 4-way conflict in the plain layout); the swizzle spreads the four rows over distinct bank quarters.  Contiguous
 // reads stay conflict-free (the map permutes bits 0-4 within every aligned run of 32), and bits >= 6 are untouched,
 // so offsets that are multiples of 64 commute with it.
+// SW bit 0: the swizzled layout; bit 1: the contiguous stage twiddles (below).
 template <int SW>
 __device__ __forceinline__ int lds_idx(int n) {
-  return SW ? (n ^ (((n >> 4) & 3) << 2)) : n;
+  return (SW & 1) ? (n ^ (((n >> 4) & 3) << 2)) : n;
 }
-// With SW, the stage twiddles w1 = tw[k (N / (Ls R))] of the stages with 4 <= Ls and a table stride > 1 are also
+// With SW bit 1, the stage twiddles w1 = tw[k (N / (Ls R))] of the stages with 4 <= Ls and a table stride > 1 are also
 // held contiguously in k after the main table (tw[N + (Ls - 4) / 3 + k], Ls = 4, 16, 64, N <= 1024;
 // tw_entries<N, 1>): a strided read of the main table puts up to 16 distinct addresses of a lane group on one or
 // two banks.
@@ -201,7 +202,7 @@ __device__ __forceinline__ void stockham_stage(const float2* __restrict__ in, fl
       if (Ls > 1) {
 #if DVH_TW_RECUR
         // one table read per butterfly, powers by recurrence (LDS reads are the scarcer resource)
-        const float2 w1 = (SW && TWS > 1) ? tw[N + (Ls - 4) / 3 + k] : tw[k * TWS];
+        const float2 w1 = ((SW & 2) && TWS > 1) ? tw[N + (Ls - 4) / 3 + k] : tw[k * TWS];
         float2 wt = w1;
 #pragma unroll
         for (int t = 1; t < R; ++t) {
@@ -257,7 +258,7 @@ template <> struct FftPlan<1024> { using T = Stockham<1024, 1, 4, 4, 4, 4, 4>; }
 template <> struct FftPlan<2048> { using T = Stockham<2048, 1, 4, 4, 4, 4, 4, 2>; };
 
 // Block-cooperative twiddle table tw[m] = exp(-2*pi*i*m/N), computed in double then rounded; with SW also the
-// contiguous stage tables of stockham_stage<..., SW = 1> (the same values: entry (Ls, k) is tw[k N / (4 Ls)]).
+// contiguous stage tables of stockham_stage<..., SW & 2> (the same values: entry (Ls, k) is tw[k N / (4 Ls)]).
 template <int N, int SW = 0>
 __device__ __forceinline__ void init_twiddles(float2* tw) {
   for (int e = threadIdx.x; e < tw_entries<N, SW>(); e += blockDim.x) {

@@ -847,7 +847,13 @@ struct EngF500 : FusedOps<EngF500, 8, 5> {
 // Half-spectrum slots per lane l (each bin f <= 512 exactly once):
 //   j = 0, 1: l, l + 256;  j = 2, 3: 256 - l, 512 - l (lane 0: 128, 384);  j = 4..7: 64 + l, 320 + l, 192 - l,
 //   448 - l;  j = 8: 512 (lane 0 only).
+#ifndef DVH_P1024_SW
+#define DVH_P1024_SW 2  // EngP1024's LDS layout / twiddles (stockham_stage SW bits): 2 = contiguous stage twiddles,
+                        // 3 = also the XOR-swizzled layout (conflict-free stores, but its per-store address XORs cost
+                        // more VALU than the conflicts: w = 499 synth10k launch 16.1 vs 15.65 ms)
+#endif
 struct EngP1024 : FusedOps<EngP1024, 8, 9> {
+  static constexpr int SW = DVH_P1024_SW;
   static constexpr int N = 1024;
   static constexpr int NFFT = 1024;
   static constexpr int NJ = 8;  // sample registers: n < N / 2
@@ -855,14 +861,14 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   static constexpr int kWaves = 4;
   static constexpr bool kNextTask = false;
   static constexpr int kTabBins = 520;  // bins f <= 512; [519].x: the slice's non-zero flag
-  // LDS layout: the swizzled one of stockham_stage<..., SW = 1> (lds_idx<1>) in both buffers, and the twiddle table
-  // with its contiguous stage tables (conflict-free twiddle reads and stage stores: the round-4 build spent 2.9 bank-
-  // conflict cycles per LDS instruction, the Ls = 4 stores and the strided twiddle reads)
-  static constexpr size_t kBlockBytes = sizeof(float2) * tw_entries<N, 1>();  // twiddle tables
+  // LDS layout (lds_idx<SW>) of both buffers and the twiddle table with its contiguous stage tables (conflict-free
+  // twiddle reads; with SW & 1 also conflict-free stage stores: the round-4 build spent 2.9 bank-conflict cycles per
+  // LDS instruction on the Ls = 4 stores and the strided twiddle reads)
+  static constexpr size_t kBlockBytes = sizeof(float2) * tw_entries<N, SW>();  // twiddle tables
   static constexpr size_t kWaveBytes = sizeof(float2) * 2 * N;                // ping-pong buffers
 
   __device__ EngP1024(char* lds, int wave, int lane_) : FusedOps<EngP1024, 8, 9>(lds, wave, lane_, N / 2) {}
-  static __device__ void block_init(char* lds) { init_twiddles<N, 1>(reinterpret_cast<float2*>(lds)); }
+  static __device__ void block_init(char* lds) { init_twiddles<N, SW>(reinterpret_cast<float2*>(lds)); }
 
   static __device__ __forceinline__ int bin(int l, int j) {
     switch (j) {
@@ -891,13 +897,13 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   }
 
   // the four outputs of radix-4 butterfly i of a span-1 stage (out[4 i + q] in the swizzled layout, whose 4-element
-  // groups stay contiguous: lds_idx<1>(4 i + q) = 4 (i ^ ((i >> 2) & 3)) + q) as two 16-byte stores at a 32-byte
+  // groups stay contiguous: lds_idx<SW>(4 i + q) = 4 i' + q) as two 16-byte stores at a 32-byte
   // lane stride; lanes with i & 4 store their second pair first so that every 8-lane store group tiles the 32 banks
   // (as EngF500's stage 1)
   static __device__ __forceinline__ void store4(float2* out, int i, float2 x0, float2 x1, float2 x2, float2 x3) {
     const bool sw = (i & 4) != 0;
     const int o = sw ? 2 : 0;
-    float4* d = reinterpret_cast<float4*>(out + lds_idx<1>(4 * i));
+    float4* d = reinterpret_cast<float4*>(out + lds_idx<SW>(4 * i));
     d[o >> 1] = sw ? make_float4(x2.x, x2.y, x3.x, x3.y) : make_float4(x0.x, x0.y, x1.x, x1.y);
     d[(2 - o) >> 1] = sw ? make_float4(x0.x, x0.y, x1.x, x1.y) : make_float4(x2.x, x2.y, x3.x, x3.y);
   }
@@ -914,7 +920,7 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
 
   // radix-4 butterfly k of the last stage (span 256): X[k + 256 q], q < 4
   __device__ __forceinline__ void last_bfly_from(const float2* src, int k, float2 (&x)[4]) const {
-    const int kb = lds_idx<1>(k);
+    const int kb = lds_idx<SW>(k);
 #pragma unroll
     for (int t = 0; t < 4; ++t) x[t] = lds_ld(src, kb + 256 * t);
     const float2 w1 = tw[k];
@@ -936,11 +942,11 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   template <class F>
   __device__ __forceinline__ void finish_with(F&& acc) const {
     wave_sync();
-    stockham_stage<N, 4, 4, 1>(bufB, bufA, tw, lane);
+    stockham_stage<N, 4, 4, SW>(bufB, bufA, tw, lane);
     wave_sync();
-    stockham_stage<N, 16, 4, 1>(bufA, bufB, tw, lane);
+    stockham_stage<N, 16, 4, SW>(bufA, bufB, tw, lane);
     wave_sync();
-    stockham_stage<N, 64, 4, 1>(bufB, bufA, tw, lane);
+    stockham_stage<N, 64, 4, SW>(bufB, bufA, tw, lane);
     wave_sync();
     const int ln = opaque(lane);  // the stage's addresses formed per call, not held in registers between calls
     const bool l0 = ln == 0;
@@ -990,13 +996,13 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
     bfly(l0 ? 128 : 192 - ln, sel(l0, A(2), A(6)), sel(l0, A(3), A(7)), sel(l0, B(3), B(5)), sel(l0, B(2), B(4)));
     bfly(l0 ? 192 : 256 - ln, sel(l0, A(6), A(2)), sel(l0, A(7), A(3)), sel(l0, B(5), B(1)), sel(l0, B(4), B(0)));
     wave_sync();
-    stockham_stage<N, 4, 4, 1>(bufB, bufA, tw, lane);
+    stockham_stage<N, 4, 4, SW>(bufB, bufA, tw, lane);
     wave_sync();
-    stockham_stage<N, 16, 4, 1>(bufA, bufB, tw, lane);
+    stockham_stage<N, 16, 4, SW>(bufA, bufB, tw, lane);
     wave_sync();
-    stockham_stage<N, 64, 4, 1>(bufB, bufA, tw, lane);
+    stockham_stage<N, 64, 4, SW>(bufB, bufA, tw, lane);
     wave_sync();
-    stockham_stage<N, 256, 4, 1>(bufA, bufB, tw, lane);
+    stockham_stage<N, 256, 4, SW>(bufA, bufB, tw, lane);
     wave_sync();
     return bufB;
   }
@@ -1011,9 +1017,9 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
 
   // (N * sum_s c_f[k], N * sum_s c_o[k]): the linear correlation folded to the circular one of period w
   __device__ float2 c(const float2* Y, int k, int w_) const {
-    float2 v = Y[lds_idx<1>(k)];
+    float2 v = Y[lds_idx<SW>(k)];
     if (k > 0) {
-      const float2 u = Y[lds_idx<1>(N - w_ + k)];
+      const float2 u = Y[lds_idx<SW>(N - w_ + k)];
       v.x += u.x;
       v.y += u.y;
     }
