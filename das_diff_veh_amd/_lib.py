@@ -43,12 +43,16 @@ SIGNATURES = {
     "dvh_ridge": [_p, _i64, _i32, _i32, _i32, _i32, _i32, _p, _i32, _f64, _f64, _p, _p, _i32, _p, _p, _p, _p],
     "dvh_sosfiltfilt_workspace": [_i64, _i32, _i32, _i32],
     "dvh_sosfiltfilt": [_p, _i32, _i64, _i64, _i32, _p, _i32, _i32, _p, _p, _p],
+    "dvh_sosfiltfilt_plan_bytes": [_i32],
+    "dvh_sosfiltfilt_plan": [_p, _i32, _p, _i32, _i32, _p, _p],
+    "dvh_sosfiltfilt_planned": [_p, _i32, _i64, _i64, _i32, _p, _i32, _i32, _p, _p, _p, _p],
     "dvh_trace_cleanup": [_p, _i32, _i64, _i64, _i32, _i32, _f64, _p, _p, _p],
     "dvh_cut_windows": [_p, _i32, _i64, _i64, _i64, _p, _i32, _i64, _i32, _i32, _p, _i32, _p, _p],
     "dvh_mute_traj": [_p, _i32, _i32, _i64, _i32, _i32, _p, _p, _p],
     "dvh_mute_time": [_p, _i32, _i64, _i32, _p, _p],
 }
-_RESTYPES = {"dvh_last_error": C.c_char_p, "dvh_vsg_stack_workspace": C.c_int64, "dvh_sosfiltfilt_workspace": C.c_int64}
+_RESTYPES = {"dvh_last_error": C.c_char_p, "dvh_vsg_stack_workspace": C.c_int64, "dvh_sosfiltfilt_workspace": C.c_int64,
+             "dvh_sosfiltfilt_plan_bytes": C.c_int64}
 
 _lock = threading.Lock()
 _lib = None

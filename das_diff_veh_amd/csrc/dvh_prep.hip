@@ -335,13 +335,13 @@ __global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* _
 }
 
 // ---------------------------------------------------------------------------------------------
-// sosfiltfilt on the float64 matrix pipe (round 5).  With blocks of kSmL = 32 samples the phases A and C above are
-// GEMMs whose operands are the block's samples and the filter's block operators, all formed on the device from the
+// sosfiltfilt on the float64 matrix pipe (round 5).  With blocks of kSmL = 64 samples the phases A and C above are
+// GEMMs whose operands are the block's samples and the filter's block operators, formed on the device from the
 // filter's own recursion (sosm_mats_kernel):
 //   h[t]       the cascade's impulse response (zero state, unit sample at step 0), t < L
 //   Hm[t][m]   its output at step t from the unit state e_m and zero input
 //   g[t][m]    its state after step t from the unit sample at step 0 (zero state)
-//   M = A^L    the zero-input transition of L samples (as sos_transition_kernel), Mzi = M zi
+//   M = A^L    the zero-input transition of L samples, Mzi = M zi, MQ = M^Q (the scan's group transition)
 // A block of L samples u_0..u_{L-1} filtered from start state s gives
 //   outputs   y_i = sum_{j <= i} h[i - j] u_j + sum_m Hm[i][m] s_m            (lower-triangular Toeplitz + L x 2NS)
 //   end state s' = M s + sum_j g[L - 1 - j] u_j                                 (2NS x L)
@@ -349,44 +349,57 @@ __global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* _
 // blocks aligned with the forward ones; the partial last forward block is the first backward block):
 //   outputs   v_i = sum_{i'' >= i} h[i'' - i] y_i'' + sum_m Hm[L - 1 - i][m] s_m  (upper-triangular Toeplitz)
 //   end state s' = M s + sum_i g[i] y_i
-// The products are v_mfma_f64_16x16x4_f64 tiles over 16 blocks (columns); the state scans between them are
-// sos_scan_kernel's.  Launches:
+// The products are v_mfma_f64_16x16x4_f64 tiles over 16 blocks (columns, 1 024 samples).  A tile's samples are moved
+// by coalesced loads (issued one tile ahead, under the previous tile's MFMAs) into an LDS image [block][sample]
+// (row stride 65 doubles: the B-operand reads are conflict-free), and its outputs leave through the same image by
+// coalesced stores.  The GEMMs fed from the image take their k index in the order sample = 16 (l >> 4) + kk, those
+// fed from accumulators (the backward end states) in the accumulator order sample = 4 kk + (l >> 4); the operator
+// (A) values are read from small LDS tables (h zero-extended for the Toeplitz factors, Hm, g) by lane-constant
+// offsets.  Launches:
+//   sosm_mats   the operators (one wave per record)
 //   sosm_fa     forward zero-state end states E_f (block 0 plus M zi x_ext[0]: its true end state)
-//   scan        true forward end states
-//   sosm_fc     forward outputs y from the true start states, written once, and from the same registers the
+//   sosm_scan   true forward end states (two-level, below)
+//   sosm_fc     forward outputs y from the true start states, written once, and from the same accumulators the
 //               backward zero-state end states E_b of every full block (the backward phase A, fused)
-//   sosm_bf     the first backward block (the partial last forward block) by the recursion, one lane per row:
-//               its outputs and the backward state after it
-//   scan        true backward end states
-//   sosm_bc     backward outputs from the true start states, trimmed to the row
-// The outputs equal the recursion's up to rounding (sums of <= 52 products per output instead of the cascade's
-// chain); tests/test_prep_gpu.py holds them to scipy.signal.sosfiltfilt at 1e-10 (float64) / 2e-6 (float32).
-constexpr int kSmL = 32;                  // samples per block: two 16-row MFMA tiles
+//   sosm_bf     the first backward block (the partial last forward block) by the recursion, one lane per row
+//   sosm_scan   true backward end states
+//   sosm_bc     backward outputs from the true start states, trimmed into the row
+// The outputs equal the recursion's up to rounding (sums of <= 84 products per output instead of the cascade's chain;
+// a float64 model of this scheme matches scipy.signal.sosfiltfilt to 1e-13); tests/test_prep_gpu.py holds them to
+// scipy at 1e-10 (float64) / 2e-6 (float32).
+constexpr int kSmL = 64;     // samples per block: four 16-row MFMA tiles
+constexpr int kSmLd = 66;    // LDS image row stride (doubles): B-operand reads (column li, sample 4 kk + q) of 32
+                             // lanes hit 32 distinct banks (2 li + q)
+constexpr int kSmRows = 32;  // state rows of the MFMA tiles (2 NS <= 32)
 typedef double doublex4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ doublex4_t mfma_f64x4(double a, double b, doublex4_t c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// offsets (doubles) of the filter operators in the MFMA path's table
+// offsets (doubles) of the filter operators in the MFMA path's table (the "plan")
 template <int NS>
 struct SosmMats {
   static constexpr int NST = 2 * NS;
   static constexpr int h = 0, Hm = kSmL, g = Hm + kSmL * NST, M = g + kSmL * NST, Mzi = M + NST * NST,
                        MQ = Mzi + NST, size = MQ + NST * NST;
 };
+constexpr int64_t sosm_plan_doubles(int n_sec) {
+  return kSmL + 2 * kSmL * (2 * n_sec) + 2 * (2 * n_sec) * (2 * n_sec) + 2 * n_sec;
+}
 
-// Experiments e < NST: unit state e_e, zero input (Hm[:, e], M[:, e], and MQ[:, e] = (A^L)^Q e_e after Q L steps,
-// the scan's group transition); e = NST: zero state, unit sample (h, g).
+// Lanes e < NST: unit state e_e, zero input (Hm[:, e], M[:, e]); lane NST: zero state, unit sample (h, g).  Then
+// Mzi = M zi and MQ = M^Q by repeated products (threads (row, col) of the 20 x 20 result, LDS).
 template <int NS>
-__global__ __launch_bounds__(64) void sosm_mats_kernel(const double* __restrict__ sos, const double* __restrict__ zi,
-                                                       int32_t Q, double* __restrict__ mats) {
+__global__ __launch_bounds__(512) void sosm_mats_kernel(const double* __restrict__ sos, const double* __restrict__ zi,
+                                                        int32_t Q, double* __restrict__ mats) {
   using O = SosmMats<NS>;
   constexpr int NST = 2 * NS;
+  __shared__ double P[NST * NST], R[NST * NST];
   const int e = threadIdx.x;
-  SosCoef<NS> c;
-  c.load(sos);
   if (e <= NST) {
+    SosCoef<NS> c;
+    c.load(sos);
     double z0[NS], z1[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -409,23 +422,44 @@ __global__ __launch_bounds__(64) void sosm_mats_kernel(const double* __restrict_
     if (e < NST) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        mats[O::M + (2 * s) * NST + e] = z0[s];
-        mats[O::M + (2 * s + 1) * NST + e] = z1[s];
-      }
-      for (int t = kSmL; t < Q * kSmL; ++t) c.step(z0, z1, 0.0);
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        mats[O::MQ + (2 * s) * NST + e] = z0[s];
-        mats[O::MQ + (2 * s + 1) * NST + e] = z1[s];
+        P[(2 * s) * NST + e] = z0[s];
+        P[(2 * s + 1) * NST + e] = z1[s];
       }
     }
   }
   __syncthreads();
+  const int row = e / NST, col = e % NST;
+  const bool act = e < NST * NST;
+  if (act) {
+    mats[O::M + e] = P[e];
+    R[e] = row == col ? 1.0 : 0.0;  // R = M^0
+  }
   if (e < NST) {
     double a = 0.0;
-    for (int j = 0; j < NST; ++j) a += mats[O::M + e * NST + j] * zi[j];
+    for (int j = 0; j < NST; ++j) a += P[e * NST + j] * zi[j];
     mats[O::Mzi + e] = a;
   }
+  // MQ = M^Q by binary powering: R *= P when the bit is set, P = P P
+  for (int q = Q; q > 0; q >>= 1) {
+    __syncthreads();
+    if (q & 1) {
+      double a = 0.0;
+      if (act)
+        for (int j = 0; j < NST; ++j) a += R[row * NST + j] * P[j * NST + col];
+      __syncthreads();
+      if (act) R[e] = a;
+      __syncthreads();
+    }
+    if (q > 1) {
+      double a = 0.0;
+      if (act)
+        for (int j = 0; j < NST; ++j) a += P[row * NST + j] * P[j * NST + col];
+      __syncthreads();
+      if (act) P[e] = a;
+    }
+  }
+  __syncthreads();
+  if (act) mats[O::MQ + e] = R[e];
 }
 
 // sample i of row r of the forward pass's sequence: the odd extension of x (0 past n_ext)
@@ -439,143 +473,290 @@ __device__ __forceinline__ double sosm_ext(const T* __restrict__ x, const SosGeo
   return 2.0 * (double)row[G.n_t - 1] - (double)row[2 * (G.n_t - 1) - j];
 }
 
-// The block operators as MFMA A operands, staged in LDS per block: lane l of k-step kk of row tile t holds
-// A[16 t + (l & 15)][4 kk + (l >> 4)].  op: 0 = G (forward end state, rows = states, k = samples), 1 = T (lower
-// Toeplitz), 2 = U (upper Toeplitz), 3 = Gb (backward end state), 4 = Hm (rows = samples, k = states), 5 = Hm
-// reversed in time.  Zero outside the operator (states >= NST).
+// Operator tables in LDS, laid out so that the lane-constant A-operand reads of a 32-lane group spread over the banks
+// (k index = sample 4 kk + q, or state KS q + q'):
+//   hq[q][64 + d] = h[d] (0 for d < 0) and hr[q][64 + d] = h[-d], one copy per lane group q at stride 145: the
+//     Toeplitz factors T[i][j] = h[i - j] = hq[q][64 + i - j] and U[i][j] = h[j - i] = hr[q][64 + i - j]
+//   hm[i][m] = Hm[i][m], stride 21;  ga[j][m] = g[L - 1 - j][m], stride 48;  gb[m][i] = g[i][m], stride 66
+//   (rows m >= 2 NS zero)
+constexpr int kHq = 145, kHmLd = 21, kGaLd = 48, kGbLd = 66;
 template <int NS>
-__device__ __forceinline__ double sosm_op(const double* __restrict__ mats, int op, int t, int kk, int l) {
+__device__ __forceinline__ void sosm_tables(const double* __restrict__ mats, double* hq, double* hr, double* hm, double* ga,
+                                            double* gb) {
   using O = SosmMats<NS>;
   constexpr int NST = 2 * NS;
-  const int row = 16 * t + (l & 15), k = 4 * kk + (l >> 4);
-  switch (op) {
-    case 0: return row < NST ? mats[O::g + (kSmL - 1 - k) * NST + row] : 0.0;
-    case 1: return row >= k ? mats[O::h + row - k] : 0.0;
-    case 2: return k >= row ? mats[O::h + k - row] : 0.0;
-    case 3: return row < NST ? mats[O::g + k * NST + row] : 0.0;
-    case 4: return k < NST ? mats[O::Hm + row * NST + k] : 0.0;
-    default: return k < NST ? mats[O::Hm + (kSmL - 1 - row) * NST + k] : 0.0;
+  for (int v = threadIdx.x; v < 4 * kHq; v += blockDim.x) {
+    const int d = v % kHq - kSmL;
+    if (hq) hq[v] = (d >= 0 && d < kSmL) ? mats[O::h + d] : 0.0;
+    if (hr) hr[v] = (d <= 0 && -d < kSmL) ? mats[O::h - d] : 0.0;
+  }
+  if (hm)
+    for (int v = threadIdx.x; v < kSmL * kHmLd; v += blockDim.x) {
+      const int i = v / kHmLd, m = v % kHmLd;
+      hm[v] = m < NST ? mats[O::Hm + i * NST + m] : 0.0;
+    }
+  if (ga)
+    for (int v = threadIdx.x; v < kSmL * kGaLd; v += blockDim.x) {
+      const int j = v / kGaLd, m = v % kGaLd;
+      ga[v] = m < NST ? mats[O::g + (kSmL - 1 - j) * NST + m] : 0.0;
+    }
+  if (gb)
+    for (int v = threadIdx.x; v < kSmRows * kGbLd; v += blockDim.x) {
+      const int m = v / kGbLd, i = v % kGbLd;
+      gb[v] = (m < NST && i < kSmL) ? mats[O::g + i * NST + m] : 0.0;
+    }
+}
+
+// A tile: 16 consecutive columns c0 .. c0 + 15 of an [n_rows][ncpr] column grid (block k of row r = column r ncpr + k;
+// 32-bit: the host checks n_rows * nb < 2^31).  Its 1 024 samples in registers: lane l, step u holds sample l of
+// column u (the LDS image [column][sample] is filled from these).
+struct SosmTile {
+  int c0, r0, k0;
+  bool one_row;  // all 16 columns in row r0
+};
+__device__ __forceinline__ SosmTile sosm_tile(int tile, int n_rows, int ncpr) {
+  SosmTile t;
+  t.c0 = tile * 16;
+  t.r0 = t.c0 / ncpr;
+  t.k0 = t.c0 - t.r0 * ncpr;
+  t.one_row = t.k0 + 16 <= ncpr && t.r0 < n_rows;
+  return t;
+}
+// (row, block) of column u of a tile
+__device__ __forceinline__ void sosm_col(const SosmTile& t, int u, int ncpr, int& r, int& k) {
+  if (t.one_row) {
+    r = t.r0;
+    k = t.k0 + u;
+  } else {
+    const int c = t.c0 + u;
+    r = c / ncpr;
+    k = c - r * ncpr;
   }
 }
 
-// the 16-column tile's column of this lane: global block g = r nb + k
-struct SosmCol {
-  int64_t g, r;
-  int k;
-  bool valid;
-};
-__device__ __forceinline__ SosmCol sosm_col(const SosGeom& G, int64_t tile, int lane) {
-  SosmCol c;
-  c.g = tile * 16 + (lane & 15);
-  c.valid = c.g < G.n_rows * G.nb;
-  c.r = c.valid ? c.g / G.nb : 0;
-  c.k = c.valid ? (int)(c.g - c.r * G.nb) : 0;
-  return c;
+// forward sequence (odd extension of x) of a tile's columns (blocks of the ext, ncpr = nb)
+template <typename T>
+__device__ __forceinline__ void sosm_load_x(const T* __restrict__ x, const SosGeom& G, const SosmTile& t, int lane,
+                                            double (&v)[16]) {
+  const int64_t e0 = (int64_t)t.k0 * kSmL;
+  if (t.one_row && e0 >= G.padlen && e0 + 16 * kSmL <= G.padlen + G.n_t) {  // interior: one contiguous run of x
+    const T* p = x + (int64_t)t.r0 * G.row_stride + (e0 - G.padlen) + lane;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = (double)p[64 * u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      int r, k;
+      sosm_col(t, u, G.nb, r, k);
+      v[u] = r < G.n_rows ? sosm_ext(x, G, r, (int64_t)k * kSmL + lane) : 0.0;
+    }
+  }
 }
 
-// Forward phase A: E_f[g] = G u_block for k < nb - 1 (block 0: + M zi u_0, its true end state).
+// forward output y of a tile's columns (ncpr = nb - 1: blocks k < nb - 1 of each row, all full)
+__device__ __forceinline__ void sosm_load_y(const double* __restrict__ y, const SosGeom& G, const SosmTile& t, int lane,
+                                            double (&v)[16]) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    int r, k;
+    sosm_col(t, u, G.nb - 1, r, k);
+    v[u] = r < G.n_rows ? y[(int64_t)r * G.n_ext + (int64_t)k * kSmL + lane] : 0.0;
+  }
+}
+
+// register samples -> the wave's LDS image [column][sample]
+__device__ __forceinline__ void sosm_to_lds(double* img, int lane, const double (&v)[16]) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) img[u * kSmLd + lane] = v[u];
+}
+
+// accumulator rows (row i = 16 t + 4 rr + (l >> 4) of column l & 15) -> the LDS image
+__device__ __forceinline__ void sosm_acc_to_lds(double* img, int lane, const doublex4_t (&acc)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) img[(lane & 15) * kSmLd + 16 * t + 4 * rr + (lane >> 4)] = acc[t][rr];
+}
+
+// state accumulators (rows m = 16 t + 4 rr + (l >> 4)) -> the LDS image as [column][NST]
+template <int NST>
+__device__ __forceinline__ void sosm_states_out(double* img, int lane, const doublex4_t (&e)[2]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = 16 * t + 4 * rr + (lane >> 4);
+      if (m < NST) img[(lane & 15) * NST + m] = e[t][rr];
+    }
+}
+
+// B operand of k-step kk (sample 4 kk + q of column li) and the Toeplitz A operands
+#define SOSM_B(kk) bsrc[4 * (kk)]
+
+// Forward phase A: E_f[c] = G u_block for k < nb - 1 (block 0: + M zi u_0, its true end state).
 template <typename T, int NS>
 __global__ __launch_bounds__(256) void sosm_fa_kernel(const T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
                                                       double* __restrict__ Sf) {
   using O = SosmMats<NS>;
-  constexpr int NST = 2 * NS, RT = (NST + 15) / 16;
-  __shared__ double opA[RT][8][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int q = threadIdx.x; q < RT * 8 * 64; q += 256) opA[q / 512][(q / 64) % 8][q % 64] = sosm_op<NS>(mats, 0, q / 512, (q / 64) % 8, q % 64);
+  constexpr int NST = 2 * NS;
+  __shared__ double ga[kSmL * kGaLd], imgs[4][16 * kSmLd];
+  sosm_tables<NS>(mats, nullptr, nullptr, nullptr, ga, nullptr);
   __syncthreads();
-  const int64_t n_tiles = (G.n_rows * G.nb + 15) / 16;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
-    const SosmCol c = sosm_col(G, tile, lane);
-    const bool full = c.valid && c.k < G.nb - 1;
-    double b[8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* img = imgs[wave];
+  const int q = lane >> 4, li = lane & 15;
+  const int nr = (int)G.n_rows;
+  const int n_tiles = (nr * G.nb + 15) / 16, stride = gridDim.x * 4;
+  int tile = blockIdx.x * 4 + wave;
+  double nx[16];
+  if (tile < n_tiles) sosm_load_x(x, G, sosm_tile(tile, nr, G.nb), lane, nx);
+  for (; tile < n_tiles; tile += stride) {
+    const SosmTile tl = sosm_tile(tile, nr, G.nb);
+    wave_barrier_lds();
+    sosm_to_lds(img, lane, nx);
+    if (tile + stride < n_tiles) sosm_load_x(x, G, sosm_tile(tile + stride, nr, G.nb), lane, nx);  // next tile
+    wave_barrier_lds();
+    doublex4_t acc[2] = {doublex4_t{0.0, 0.0, 0.0, 0.0}, doublex4_t{0.0, 0.0, 0.0, 0.0}};
+    const double* bsrc = img + li * kSmLd + q;               // B: sample 4 kk + q of column li
+    const double* asrc = ga + q * kGaLd + li;  // A: G[16 t + li][4 kk + q] = ga[4 kk + q][16 t + li]
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) b[kk] = full ? sosm_ext(x, G, c.r, (int64_t)c.k * kSmL + 4 * kk + (lane >> 4)) : 0.0;
-    doublex4_t acc[RT];
+    for (int kk = 0; kk < 16; ++kk) {
+      const double b = SOSM_B(kk);
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) acc[t] = mfma_f64x4(opA[t][kk][lane], b[kk], acc[t]);
+      for (int t = 0; t < 2; ++t) acc[t] = mfma_f64x4(asrc[4 * kk * kGaLd + 16 * t], b, acc[t]);
     }
-    const double u0 = (full && c.k == 0) ? sosm_ext(x, G, c.r, 0) : 0.0;
+    // block 0 of a row: its true end state M zi u_0 + E
+    int r, k;
+    sosm_col(tl, li, G.nb, r, k);
+    const double u0 = (k == 0 && r < nr) ? sosm_ext(x, G, r, 0) : 0.0;
+    if (__ballot(u0 != 0.0) != 0) {
 #pragma unroll
-    for (int t = 0; t < RT; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int m = 16 * t + 4 * rr + (lane >> 4);
-        if (full && m < NST) Sf[c.g * NST + m] = acc[t][rr] + u0 * mats[O::Mzi + m];
+        for (int rr = 0; rr < 4; ++rr) {
+          const int m = 16 * t + 4 * rr + q;
+          if (m < NST) acc[t][rr] += u0 * mats[O::Mzi + m];
+        }
+    }
+    wave_barrier_lds();
+    sosm_states_out<NST>(img, lane, acc);
+    wave_barrier_lds();
+    // 16 x NST states, element v = column * NST + m; only full blocks (k < nb - 1) keep an end state
+#pragma unroll
+    for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
+      const int v = lane + 64 * u;
+      if (v < 16 * NST) {
+        int rc, kc;
+        sosm_col(tl, v / NST, G.nb, rc, kc);
+        if (rc < nr && kc < G.nb - 1) Sf[((int64_t)rc * G.nb + kc) * NST + v % NST] = img[v];
       }
+    }
   }
 }
 
 // Forward phase C + backward phase A: y = T u + Hm s (s: the true start state, zi u_0 for block 0), then
-// E_b = Gb y from the same registers, stored at the backward block index nb - 1 - k (full blocks only).
+// E_b = Gb y from the accumulators, stored at the backward block index nb - 1 - k (full blocks only).
 template <typename T, int NS>
 __global__ __launch_bounds__(256) void sosm_fc_kernel(const T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
                                                       const double* __restrict__ zi, const double* __restrict__ Sf,
                                                       double* __restrict__ y, double* __restrict__ Sb) {
-  constexpr int NST = 2 * NS, RT = (NST + 15) / 16, KS = (NST + 3) / 4;
-  __shared__ double opT[2][8][64], opH[2][KS][64], opG[RT][8][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int q = threadIdx.x; q < 2 * 8 * 64; q += 256) opT[q / 512][(q / 64) % 8][q % 64] = sosm_op<NS>(mats, 1, q / 512, (q / 64) % 8, q % 64);
-  for (int q = threadIdx.x; q < 2 * KS * 64; q += 256)
-    opH[q / (KS * 64)][(q / 64) % KS][q % 64] = sosm_op<NS>(mats, 4, q / (KS * 64), (q / 64) % KS, q % 64);
-  for (int q = threadIdx.x; q < RT * 8 * 64; q += 256) opG[q / 512][(q / 64) % 8][q % 64] = sosm_op<NS>(mats, 3, q / 512, (q / 64) % 8, q % 64);
+  constexpr int NST = 2 * NS, KS = (NST + 3) / 4;
+  __shared__ double hq[4 * kHq], hm[kSmL * kHmLd], gb[kSmRows * kGbLd], imgs[4][16 * kSmLd];
+  sosm_tables<NS>(mats, hq, nullptr, hm, nullptr, gb);
   __syncthreads();
-  const int64_t n_tiles = (G.n_rows * G.nb + 15) / 16;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
-    const SosmCol c = sosm_col(G, tile, lane);
-    const int64_t i0 = (int64_t)c.k * kSmL;
-    double b[8], sv[KS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* img = imgs[wave];
+  const int q = lane >> 4, li = lane & 15;
+  const int nr = (int)G.n_rows;
+  const int n_tiles = (nr * G.nb + 15) / 16, stride = gridDim.x * 4;
+  int tile = blockIdx.x * 4 + wave;
+  // the start state of column li, states m = KS q + q' (q' < KS) in this lane: contiguous in Sf
+  auto load_s = [&](const SosmTile& t, double (&s)[KS]) {
+    int r, k;
+    sosm_col(t, li, G.nb, r, k);
+    const bool ok = r < nr;
+    const double u0 = (ok && k == 0) ? sosm_ext(x, G, r, 0) : 0.0;
+    const double* sp = Sf + ((int64_t)r * G.nb + k - 1) * NST;
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) b[kk] = c.valid ? sosm_ext(x, G, c.r, i0 + 4 * kk + (lane >> 4)) : 0.0;
-    const double u0 = (c.valid && c.k == 0) ? sosm_ext(x, G, c.r, 0) : 0.0;
-#pragma unroll
-    for (int q = 0; q < KS; ++q) {
-      const int m = 4 * q + (lane >> 4);
-      sv[q] = (!c.valid || m >= NST) ? 0.0 : (c.k == 0 ? zi[m] * u0 : Sf[(c.g - 1) * NST + m]);
+    for (int qq = 0; qq < KS; ++qq) {
+      const int m = KS * q + qq;
+      s[qq] = (!ok || m >= NST) ? 0.0 : (k == 0 ? zi[m] * u0 : sp[m]);
     }
-    doublex4_t acc[2];
+  };
+  double nx[16], ns[KS];
+  if (tile < n_tiles) {
+    const SosmTile t0 = sosm_tile(tile, nr, G.nb);
+    sosm_load_x(x, G, t0, lane, nx);
+    load_s(t0, ns);
+  }
+  for (; tile < n_tiles; tile += stride) {
+    const SosmTile tl = sosm_tile(tile, nr, G.nb);
+    double sv[KS];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < 4 * (t + 1); ++kk) acc[t] = mfma_f64x4(opT[t][kk][lane], b[kk], acc[t]);  // lower triangle
-#pragma unroll
-      for (int q = 0; q < KS; ++q) acc[t] = mfma_f64x4(opH[t][q][lane], sv[q], acc[t]);
+    for (int qq = 0; qq < KS; ++qq) sv[qq] = ns[qq];
+    wave_barrier_lds();
+    sosm_to_lds(img, lane, nx);
+    if (tile + stride < n_tiles) {  // the next tile's samples and start states, in flight under this tile's MFMAs
+      const SosmTile tn = sosm_tile(tile + stride, nr, G.nb);
+      sosm_load_x(x, G, tn, lane, nx);
+      load_s(tn, ns);
     }
-    const int64_t P = c.k == G.nb - 1 ? G.n_ext - i0 : kSmL;
-    double* yr = y + c.r * G.n_ext + i0;
+    wave_barrier_lds();
+    doublex4_t acc[4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 4; ++t) acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
+    const double* bsrc = img + li * kSmLd + q;          // B: sample 4 kk + q of column li
+    const double* tsrc = hq + q * kHq + kSmL + li - q;  // A: T[16 t + li][4 kk + q] = hq[q][64 + 16 t + li - 4 kk - q]
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int i = 16 * t + 4 * rr + (lane >> 4);
-        if (c.valid && i < P) yr[i] = acc[t][rr];
+    for (int kk = 0; kk < 16; ++kk) {
+      const double b = SOSM_B(kk);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (kk <= 4 * t + 3) acc[t] = mfma_f64x4(tsrc[16 * t - 4 * kk], b, acc[t]);  // the lower triangle's k-steps
+    }
+    const double* msrc = hm + li * kHmLd + KS * q;   // A: Hm[16 t + li][KS q + q']
+#pragma unroll
+    for (int qq = 0; qq < KS; ++qq)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = mfma_f64x4(msrc[16 * t * kHmLd + qq], sv[qq], acc[t]);
+    // backward zero-state end state Gb y: y (rows = samples) as the B operand straight from the accumulators
+    // (register rr of tile t is k-step 4 t + rr: sample 16 t + 4 rr + q)
+    doublex4_t e[2] = {doublex4_t{0.0, 0.0, 0.0, 0.0}, doublex4_t{0.0, 0.0, 0.0, 0.0}};
+    const double* gsrc = gb + li * kGbLd + q;        // A: gb[16 t' + li][4 kk + q]
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) e[t] = mfma_f64x4(gsrc[16 * t * kGbLd + 4 * kk], acc[kk >> 2][kk & 3], e[t]);
+    // y through the image: coalesced row runs
+    wave_barrier_lds();
+    sosm_acc_to_lds(img, lane, acc);
+    wave_barrier_lds();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      int r, k;
+      sosm_col(tl, u, G.nb, r, k);
+      const int64_t i = (int64_t)k * kSmL + lane;
+      if (r < nr && i < G.n_ext) y[(int64_t)r * G.n_ext + i] = img[u * kSmLd + lane];
+    }
+    // E_b of full blocks at backward index nb - 1 - k
+    wave_barrier_lds();
+    sosm_states_out<NST>(img, lane, e);
+    wave_barrier_lds();
+#pragma unroll
+    for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
+      const int v = lane + 64 * u;
+      if (v < 16 * NST) {
+        int rc, kc;
+        sosm_col(tl, v / NST, G.nb, rc, kc);
+        if (rc < nr && kc < G.nb - 1) Sb[((int64_t)rc * G.nb + (G.nb - 1 - kc)) * NST + v % NST] = img[v];
       }
-    // backward zero-state end state of this block: Gb y, y (rows = samples) as the B operand straight from the
-    // accumulators (D register rr of tile t is k-step 4 t + rr)
-    doublex4_t e[RT];
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      e[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) e[t] = mfma_f64x4(opG[t][kk][lane], acc[kk >> 2][kk & 3], e[t]);
     }
-    const bool fullb = c.valid && c.k < G.nb - 1;
-    double* sb = Sb + (c.r * G.nb + (G.nb - 1 - c.k)) * NST;
-#pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int m = 16 * t + 4 * rr + (lane >> 4);
-        if (fullb && m < NST) sb[m] = e[t][rr];
-      }
   }
 }
 
 // The first backward block (forward block nb - 1, P = n_ext - (nb - 1) L samples) by the recursion from zi y[-1],
-// one lane per row: its outputs (trimmed) and the backward state after it (Sb[r][0]).
+// one lane per row: its outputs (trimmed) and the backward state after it (Sb[r][0]).  The block's samples are loaded
+// 16 at a time ahead of the recursion that consumes them.
 template <typename T, int NS>
 __global__ __launch_bounds__(64) void sosm_bf_kernel(T* __restrict__ x, SosGeom G, const double* __restrict__ sos,
                                                      const double* __restrict__ zi, const double* __restrict__ y,
@@ -594,10 +775,19 @@ __global__ __launch_bounds__(64) void sosm_bf_kernel(T* __restrict__ x, SosGeom 
     z1[q] = zi[2 * q + 1] * ul;
   }
   const int64_t start = (int64_t)(G.nb - 1) * kSmL;
-  for (int64_t i = G.n_ext - 1; i >= start; --i) {
-    const double v = c.step(z0, z1, yr[i]);
-    const int64_t j = i - G.padlen;
-    if (j >= 0 && j < G.n_t) x[r * G.row_stride + j] = (T)v;
+  double cur[16];
+  for (int64_t i0 = G.n_ext - 1; i0 >= start; i0 -= 16) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) cur[t] = i0 - t >= start ? yr[i0 - t] : 0.0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int64_t i = i0 - t;
+      if (i >= start) {
+        const double v = c.step(z0, z1, cur[t]);
+        const int64_t j = i - G.padlen;
+        if (j >= 0 && j < G.n_t) x[r * G.row_stride + j] = (T)v;
+      }
+    }
   }
   double* sb = Sb + r * G.nb * NST;
 #pragma unroll
@@ -607,55 +797,82 @@ __global__ __launch_bounds__(64) void sosm_bf_kernel(T* __restrict__ x, SosGeom 
   }
 }
 
-// Backward phase C for backward blocks k' >= 1 (forward blocks k = nb - 1 - k' < nb - 1): v = U y + Hrev s with s
-// the true backward state before the block, written into the row (trimmed).
+// Backward phase C for backward blocks k' >= 1 (forward blocks k = nb - 1 - k' < nb - 1, columns (r, k) of an
+// [n_rows][nb - 1] grid): v = U y + Hrev s with s the true backward state before the block, trimmed into the row.
 template <typename T, int NS>
 __global__ __launch_bounds__(256) void sosm_bc_kernel(T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
                                                       const double* __restrict__ y, const double* __restrict__ Sb) {
   constexpr int NST = 2 * NS, KS = (NST + 3) / 4;
-  __shared__ double opU[2][8][64], opH[2][KS][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int q = threadIdx.x; q < 2 * 8 * 64; q += 256) opU[q / 512][(q / 64) % 8][q % 64] = sosm_op<NS>(mats, 2, q / 512, (q / 64) % 8, q % 64);
-  for (int q = threadIdx.x; q < 2 * KS * 64; q += 256)
-    opH[q / (KS * 64)][(q / 64) % KS][q % 64] = sosm_op<NS>(mats, 5, q / (KS * 64), (q / 64) % KS, q % 64);
+  __shared__ double hr[4 * kHq], hm[kSmL * kHmLd], imgs[4][16 * kSmLd];
+  sosm_tables<NS>(mats, nullptr, hr, hm, nullptr, nullptr);
   __syncthreads();
-  // columns: (r, k) with k < nb - 1, i.e. nb - 1 per row
-  const int nbc = G.nb - 1;
-  const int64_t n_cols = G.n_rows * nbc, n_tiles = (n_cols + 15) / 16;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < n_tiles; tile += (int64_t)gridDim.x * 4) {
-    const int64_t g = tile * 16 + (lane & 15);
-    const bool valid = g < n_cols;
-    const int64_t r = valid ? g / nbc : 0;
-    const int k = valid ? (int)(g - r * nbc) : 0;
-    const double* yr = y + r * G.n_ext + (int64_t)k * kSmL;
-    double b[8], sv[KS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* img = imgs[wave];
+  const int q = lane >> 4, li = lane & 15;
+  const int nr = (int)G.n_rows, nc = G.nb - 1;
+  const int n_tiles = (nr * nc + 15) / 16, stride = gridDim.x * 4;
+  int tile = blockIdx.x * 4 + wave;
+  auto load_s = [&](const SosmTile& t, double (&s)[KS]) {  // backward state before block k: Sb[r][nb - 2 - k]
+    int r, k;
+    sosm_col(t, li, nc, r, k);
+    const bool ok = r < nr;
+    const double* sp = Sb + ((int64_t)r * G.nb + (G.nb - 2 - k)) * NST;
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) b[kk] = valid ? yr[4 * kk + (lane >> 4)] : 0.0;
-    const double* sb = Sb + (r * G.nb + (G.nb - 2 - k)) * NST;  // backward block k' - 1 = nb - 2 - k
-#pragma unroll
-    for (int q = 0; q < KS; ++q) {
-      const int m = 4 * q + (lane >> 4);
-      sv[q] = (valid && m < NST) ? sb[m] : 0.0;
+    for (int qq = 0; qq < KS; ++qq) {
+      const int m = KS * q + qq;
+      s[qq] = (ok && m < NST) ? sp[m] : 0.0;
     }
-    doublex4_t acc[2];
+  };
+  double ny[16], ns[KS];
+  if (tile < n_tiles) {
+    const SosmTile t0 = sosm_tile(tile, nr, nc);
+    sosm_load_y(y, G, t0, lane, ny);
+    load_s(t0, ns);
+  }
+  for (; tile < n_tiles; tile += stride) {
+    const SosmTile tl = sosm_tile(tile, nr, nc);
+    double sv[KS];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 4 * t; kk < 8; ++kk) acc[t] = mfma_f64x4(opU[t][kk][lane], b[kk], acc[t]);  // upper triangle
-#pragma unroll
-      for (int q = 0; q < KS; ++q) acc[t] = mfma_f64x4(opH[t][q][lane], sv[q], acc[t]);
+    for (int qq = 0; qq < KS; ++qq) sv[qq] = ns[qq];
+    wave_barrier_lds();
+    sosm_to_lds(img, lane, ny);
+    if (tile + stride < n_tiles) {
+      const SosmTile tn = sosm_tile(tile + stride, nr, nc);
+      sosm_load_y(y, G, tn, lane, ny);
+      load_s(tn, ns);
     }
-    T* xr = x + r * G.row_stride;
+    wave_barrier_lds();
+    doublex4_t acc[4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 4; ++t) acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
+    const double* bsrc = img + li * kSmLd + q;          // B: sample 4 kk + q of column li
+    const double* usrc = hr + q * kHq + kSmL + li - q;  // A: U[16 t + li][4 kk + q] = hr[q][64 + 16 t + li - 4 kk - q]
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int64_t j = (int64_t)k * kSmL + 16 * t + 4 * rr + (lane >> 4) - G.padlen;
-        if (valid && j >= 0 && j < G.n_t) xr[j] = (T)acc[t][rr];
-      }
+    for (int kk = 0; kk < 16; ++kk) {
+      const double b = SOSM_B(kk);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (kk >= 4 * t) acc[t] = mfma_f64x4(usrc[16 * t - 4 * kk], b, acc[t]);  // the upper triangle's k-steps
+    }
+    const double* msrc = hm + (kSmL - 1 - li) * kHmLd + KS * q;  // A: Hm[L - 1 - (16 t + li)][KS q + q']
+#pragma unroll
+    for (int qq = 0; qq < KS; ++qq)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = mfma_f64x4(msrc[-16 * t * kHmLd + qq], sv[qq], acc[t]);
+    wave_barrier_lds();
+    sosm_acc_to_lds(img, lane, acc);
+    wave_barrier_lds();
+    // v at ext index k L + i -> x[j = k L + i - padlen] when 0 <= j < n_t
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      int r, k;
+      sosm_col(tl, u, nc, r, k);
+      const int64_t j = (int64_t)k * kSmL + lane - G.padlen;
+      if (r < nr && j >= 0 && j < G.n_t) x[(int64_t)r * G.row_stride + j] = (T)img[u * kSmLd + lane];
+    }
   }
 }
+#undef SOSM_B
 
 // The state scan S[k] = S[k] + M S[k - 1], k = 1 .. K - 1 (K = nb - 1 end states; S[0] already true; S[k] holds
 // the zero-state end state E[k] on entry), two-level: one 512-thread block per row, 16 half-waves (lane j = state
@@ -663,9 +880,9 @@ __global__ __launch_bounds__(256) void sosm_bc_kernel(T* __restrict__ x, SosGeom
 //   1  every group runs the scan from a zero start (group 0 from S[0]): Z[k] = E[k] + M Z[k - 1] (into S[k]);
 //   2  the carries, in order: C_q = Z[last of q] + M^Q C_{q - 1} (C_0 = Z[last of 0], already true);
 //   3  every group q >= 1 adds the carried part: D = M D from D = C_{q - 1}, S[k] = Z[k] + D.
-// 2 Q + NG dependent steps instead of K - 1 (record of 1 024 x 60 s: 76 instead of 471).  M^Q is formed by the
-// recursion (sosm_mats_kernel).
-constexpr int kScanHW = 16;
+// 2 Q + NG dependent steps instead of K - 1 (record of 1 024 x 60 s: 46 instead of 235).  A group's operands are
+// loaded kScanPF steps at a time, in one batch ahead of the steps that use them.
+constexpr int kScanHW = 16, kScanPF = 16;
 __host__ __device__ constexpr int sosm_scan_q(int nb) { return nb > 2 ? (nb - 2 + kScanHW - 1) / kScanHW : 1; }
 
 template <int NS>
@@ -674,19 +891,14 @@ __global__ __launch_bounds__(512) void sosm_scan_kernel(SosGeom G, const double*
   using O = SosmMats<NS>;
   constexpr int NST = 2 * NS;
   __shared__ __attribute__((aligned(16))) double sv[kScanHW][32];
-  __shared__ double carry[kScanHW][NST];
+  __shared__ double carry[kScanHW][NST], zlast[kScanHW][NST], mqs[NST * NST];
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   const bool act = j < NST;
-  const int64_t r = blockIdx.x;
-  double* Sr = S + r * (int64_t)G.nb * NST;
+  double* Sr = S + (int64_t)blockIdx.x * G.nb * NST;
   const int K = G.nb - 1;
   const int k0 = 1 + hw * Q, k1 = min(1 + (hw + 1) * Q, K);  // this half-wave's group [k0, k1)
-  // one matvec step: out_j = add + sum_i A[j][i] x_i, x from this half-wave's LDS slot (every lane of the wave runs
-  // the same steps; lanes of an empty group compute on zeros)
-  double m[NST];
-#pragma unroll
-  for (int i = 0; i < NST; ++i) m[i] = act ? mats[O::M + j * NST + i] : 0.0;
-  auto matvec = [&](const double (&A)[NST], double add) {
+  const int ng = K > 1 ? (K - 1 + Q - 1) / Q : 0;              // non-empty groups
+  auto matvec = [&](const double* A, double add) {  // add + sum_i A[i] x_i (row j of the matrix), x from the LDS slot
     wave_barrier_lds();
     const double2* v2 = reinterpret_cast<const double2*>(sv[hw]);
     double pa[4] = {add, 0.0, 0.0, 0.0};
@@ -698,47 +910,61 @@ __global__ __launch_bounds__(512) void sosm_scan_kernel(SosGeom G, const double*
     }
     return (pa[0] + pa[1]) + (pa[2] + pa[3]);
   };
-  // level 1: zero-start scans of the groups (group 0 from the true S[0])
-  double z = (hw == 0 && act) ? Sr[j] : 0.0;
-  sv[hw][j] = z;
-  const int nmax = Q;  // every half-wave runs Q steps; those past its group compute on zeros and store nothing
-  double e = (act && k0 < k1) ? Sr[(int64_t)k0 * NST + j] : 0.0;
-  for (int t = 0; t < nmax; ++t) {
-    const int k = k0 + t;
-    const double en = (act && k + 1 < k1) ? Sr[(int64_t)(k + 1) * NST + j] : 0.0;  // the next E under this step
-    z = matvec(m, e);
-    if (act && k < k1) Sr[(int64_t)k * NST + j] = z;
+  auto put = [&](double v) {
     wave_barrier_lds();
-    sv[hw][j] = z;
-    e = en;
+    sv[hw][j] = v;
+  };
+  double m[NST];
+#pragma unroll
+  for (int i = 0; i < NST; ++i) m[i] = act ? mats[O::M + j * NST + i] : 0.0;
+  // level 1: zero-start scans of the groups (group 0 from the true S[0])
+  put((hw == 0 && act) ? Sr[j] : 0.0);
+  double cur[kScanPF];
+  for (int kb = k0; kb < k0 + Q; kb += kScanPF) {
+#pragma unroll
+    for (int t = 0; t < kScanPF; ++t) cur[t] = (act && kb + t < k1) ? Sr[(int64_t)(kb + t) * NST + j] : 0.0;
+#pragma unroll
+    for (int t = 0; t < kScanPF; ++t) {
+      const int k = kb + t;
+      if (k < k0 + Q) {  // every half-wave runs Q steps (lanes past their group compute on zeros, store nothing)
+        const double z = matvec(m, cur[t]);
+        if (act && k < k1) Sr[(int64_t)k * NST + j] = z;
+        if (act && k == k1 - 1) zlast[hw][j] = z;  // the group's last Z, for the carries
+        cur[t] = z;
+        put(z);
+      }
+    }
   }
-  // the group's last Z is in sv[hw] (steps past the group keep z = M^t Z_last + 0: they do not, so keep it apart)
+  for (int v = threadIdx.x; v < NST * NST; v += blockDim.x) mqs[v] = mats[O::MQ + v];
   __syncthreads();
-  const int ng = K > 1 ? (K - 1 + Q - 1) / Q : 0;  // non-empty groups
   // level 2: carries by one half-wave
   if (hw == 0) {
-    double mq[NST];
-#pragma unroll
-    for (int i = 0; i < NST; ++i) mq[i] = act ? mats[O::MQ + j * NST + i] : 0.0;
-    double c = (act && ng > 0) ? Sr[(int64_t)(min(1 + Q, K) - 1) * NST + j] : 0.0;  // C_0 = S[last of group 0]
+    double c = act ? zlast[0][j] : 0.0;
     if (act) carry[0][j] = c;
-    for (int q = 1; q + 1 < ng; ++q) {
-      wave_barrier_lds();
-      sv[0][j] = c;
-      const double zl = act ? Sr[(int64_t)(min(1 + (q + 1) * Q, K) - 1) * NST + j] : 0.0;
-      c = matvec(mq, zl);
-      if (act) carry[q][j] = c;
+    for (int g = 1; g + 1 < ng; ++g) {
+      put(c);
+      c = matvec(mqs + (act ? j : 0) * NST, act ? zlast[g][j] : 0.0);
+      if (act) carry[g][j] = c;
     }
   }
   __syncthreads();
-  // level 3: the carried part of groups q >= 1
+  // level 3: the carried part of groups q >= 1 (Z from the registers when the group fits one batch)
   if (hw >= 1 && hw < ng) {
     double d = act ? carry[hw - 1][j] : 0.0;
-    for (int k = k0; k < k1; ++k) {
-      wave_barrier_lds();
-      sv[hw][j] = d;
-      d = matvec(m, 0.0);
-      if (act) Sr[(int64_t)k * NST + j] += d;
+    for (int kb = k0; kb < k1; kb += kScanPF) {
+      if (Q > kScanPF) {
+#pragma unroll
+        for (int t = 0; t < kScanPF; ++t) cur[t] = (act && kb + t < k1) ? Sr[(int64_t)(kb + t) * NST + j] : 0.0;
+      }
+#pragma unroll
+      for (int t = 0; t < kScanPF; ++t) {
+        const int k = kb + t;
+        if (k < k1) {
+          put(d);
+          d = matvec(m, 0.0);
+          if (act) Sr[(int64_t)k * NST + j] = cur[t] + d;
+        }
+      }
     }
   }
 }
@@ -755,37 +981,56 @@ static SosGeom sosm_geom(int64_t n_rows, int64_t row_stride, int32_t n_t, int32_
   return G;
 }
 
-// workspace of the MFMA path: y [n_rows][n_ext] + Sf, Sb [n_rows][nb][2 n_sec] + the operator table, doubles
+// workspace of the MFMA path: y [n_rows][n_ext] + Sf, Sb [n_rows][nb][2 n_sec] + the plan (operator table), doubles
 static int64_t sosm_workspace_doubles(const SosGeom& G, int n_sec) {
   const int64_t nst = 2 * n_sec;
-  return G.n_rows * G.n_ext + 2 * G.n_rows * G.nb * nst + (kSmL + 2 * kSmL * nst + 2 * nst * nst + nst);
+  return G.n_rows * G.n_ext + 2 * G.n_rows * G.nb * nst + sosm_plan_doubles(n_sec);
+}
+// the MFMA path's column indices are 32-bit
+static bool sosm_fits(const SosGeom& G) { return G.n_rows * (int64_t)G.nb < (1LL << 31) - 16; }
+
+template <int NS>
+static void sosm_plan(const double* sos, const double* zi, const SosGeom& G, double* plan, hipStream_t st) {
+  hipLaunchKernelGGL(sosm_mats_kernel<NS>, dim3(1), dim3(512), 0, st, sos, zi, (int32_t)sosm_scan_q(G.nb), plan);
 }
 
 template <typename T, int NS>
-static int sosfiltfilt_mfma(T* x, const SosGeom& G, const double* sos, const double* zi, double* work, hipStream_t st) {
+static int sosm_run(T* x, const SosGeom& G, const double* sos, const double* zi, const double* plan, double* work,
+                    hipStream_t st) {
   constexpr int NST = 2 * NS;
   double* y = work;
   double* Sf = y + G.n_rows * G.n_ext;
   double* Sb = Sf + G.n_rows * G.nb * NST;
-  double* mats = Sb + G.n_rows * G.nb * NST;
-  const int64_t tiles = (G.n_rows * G.nb + 15) / 16;
-  const unsigned grid = (unsigned)std::min<int64_t>((tiles + 3) / 4, 65535);
   const int Q = sosm_scan_q(G.nb);
-  hipLaunchKernelGGL(sosm_mats_kernel<NS>, dim3(1), dim3(64), 0, st, sos, zi, Q, mats);
-  if (G.nb > 1) hipLaunchKernelGGL((sosm_fa_kernel<T, NS>), dim3(grid), dim3(256), 0, st, (const T*)x, G, (const double*)mats, Sf);
-  if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, (const double*)mats, Q, Sf);
-  hipLaunchKernelGGL((sosm_fc_kernel<T, NS>), dim3(grid), dim3(256), 0, st, (const T*)x, G, (const double*)mats, zi,
+  // persistent-ish grids: at most 2 048 four-wave blocks, each wave looping over tiles
+  auto grid_of = [](int64_t tiles) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 2048)); };
+  const int64_t tiles = (G.n_rows * G.nb + 15) / 16;
+  if (G.nb > 1) hipLaunchKernelGGL((sosm_fa_kernel<T, NS>), dim3(grid_of(tiles)), dim3(256), 0, st, (const T*)x, G, plan, Sf);
+  if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, plan, Q, Sf);
+  hipLaunchKernelGGL((sosm_fc_kernel<T, NS>), dim3(grid_of(tiles)), dim3(256), 0, st, (const T*)x, G, plan, zi,
                      (const double*)Sf, y, Sb);
   hipLaunchKernelGGL((sosm_bf_kernel<T, NS>), dim3((unsigned)((G.n_rows + 63) / 64)), dim3(64), 0, st, x, G, sos, zi,
                      (const double*)y, Sb);
   if (G.nb > 1) {
-    if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, (const double*)mats, Q, Sb);
+    if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, plan, Q, Sb);
     const int64_t tb = (G.n_rows * (G.nb - 1) + 15) / 16;
-    hipLaunchKernelGGL((sosm_bc_kernel<T, NS>), dim3((unsigned)std::min<int64_t>((tb + 3) / 4, 65535)), dim3(256), 0, st, x, G,
-                       (const double*)mats, (const double*)y, (const double*)Sb);
+    hipLaunchKernelGGL((sosm_bc_kernel<T, NS>), dim3(grid_of(tb)), dim3(256), 0, st, x, G, plan, (const double*)y,
+                       (const double*)Sb);
   }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
+}
+
+// plan == nullptr: formed into the workspace's tail first (dvh_sosfiltfilt); else the caller's (dvh_sosfiltfilt_planned)
+template <typename T, int NS>
+static int sosfiltfilt_mfma(T* x, const SosGeom& G, const double* sos, const double* zi, const double* plan, double* work,
+                            hipStream_t st) {
+  if (!plan) {
+    double* p = work + G.n_rows * G.n_ext + 2 * G.n_rows * G.nb * (2 * NS);
+    sosm_plan<NS>(sos, zi, G, p, st);
+    plan = p;
+  }
+  return sosm_run<T, NS>(x, G, sos, zi, plan, work, st);
 }
 
 // block length: enough (row, block) lanes for ~4 waves per SIMD, blocks of 32 .. 4096 samples
@@ -837,15 +1082,17 @@ static int sosfiltfilt_blocks(T* x, const SosGeom& G, const double* sos, const d
 }
 
 #ifndef DVH_SOS_MFMA
-#define DVH_SOS_MFMA 0  // sosfiltfilt's block phases as float64 MFMA GEMMs (0: the VALU recursion per (row, block) lane)
+#define DVH_SOS_MFMA 1  // sosfiltfilt's block phases as float64 MFMA GEMMs (0: the VALU recursion per (row, block) lane)
 #endif
 
+// MFMA path (when it fits its 32-bit column indices) or the VALU block recursion
 template <typename T>
-static int sosfiltfilt_dispatch(T* x, const SosGeom& G, const double* sos, int n_sec, const double* zi, double* work,
-                                hipStream_t st) {
+static int sosfiltfilt_dispatch(T* x, const SosGeom& Gm, const SosGeom& Gb, const double* sos, int n_sec, const double* zi,
+                                const double* plan, double* work, hipStream_t st) {
+  const bool mf = DVH_SOS_MFMA && sosm_fits(Gm);
   switch (n_sec) {
 #define DVH_SOS_CASE(n) \
-  case n: return DVH_SOS_MFMA ? sosfiltfilt_mfma<T, n>(x, G, sos, zi, work, st) : sosfiltfilt_blocks<T, n>(x, G, sos, zi, work, st);
+  case n: return mf ? sosfiltfilt_mfma<T, n>(x, Gm, sos, zi, plan, work, st) : sosfiltfilt_blocks<T, n>(x, Gb, sos, zi, work, st);
     DVH_SOS_CASE(1) DVH_SOS_CASE(2) DVH_SOS_CASE(3) DVH_SOS_CASE(4) DVH_SOS_CASE(5) DVH_SOS_CASE(6)
     DVH_SOS_CASE(7) DVH_SOS_CASE(8) DVH_SOS_CASE(9) DVH_SOS_CASE(10) DVH_SOS_CASE(11) DVH_SOS_CASE(12)
     DVH_SOS_CASE(13) DVH_SOS_CASE(14) DVH_SOS_CASE(15) DVH_SOS_CASE(16)
@@ -1044,8 +1291,31 @@ DVH_API int dvh_trace_cleanup(void* x, int32_t dtype, int64_t n_rows, int64_t ro
 
 DVH_API int64_t dvh_sosfiltfilt_workspace(int64_t n_rows, int32_t n_t, int32_t n_sec, int32_t padlen) {
   if (n_rows <= 0 || n_t <= 0 || n_sec <= 0 || n_sec > kMaxSec || padlen < 0) return 0;
-  return 8 * (DVH_SOS_MFMA ? sosm_workspace_doubles(sosm_geom(n_rows, n_t, n_t, padlen), n_sec)
-                           : sos_workspace_doubles(sos_geom(n_rows, n_t, n_t, padlen), n_sec));
+  return 8 * std::max(sosm_workspace_doubles(sosm_geom(n_rows, n_t, n_t, padlen), n_sec),
+                      sos_workspace_doubles(sos_geom(n_rows, n_t, n_t, padlen), n_sec));
+}
+
+DVH_API int64_t dvh_sosfiltfilt_plan_bytes(int32_t n_sec) {
+  if (n_sec <= 0 || n_sec > kMaxSec) return 0;
+  return 8 * sosm_plan_doubles(n_sec);
+}
+
+DVH_API int dvh_sosfiltfilt_plan(const double* sos, int32_t n_sec, const double* zi, int32_t n_t, int32_t padlen,
+                                 double* plan, void* stream) {
+  if (!sos || !zi || !plan) return set_error(-2, "null pointer argument");
+  if (n_sec <= 0 || n_sec > kMaxSec) return set_error(-4, "unsupported number of second-order sections");
+  if (padlen < 0 || n_t < 2) return set_error(-2, "invalid padlen / length");
+  const SosGeom G = sosm_geom(1, n_t, n_t, padlen);
+  switch (n_sec) {
+#define DVH_SOS_PLAN(n) \
+  case n: sosm_plan<n>(sos, zi, G, plan, (hipStream_t)stream); break;
+    DVH_SOS_PLAN(1) DVH_SOS_PLAN(2) DVH_SOS_PLAN(3) DVH_SOS_PLAN(4) DVH_SOS_PLAN(5) DVH_SOS_PLAN(6)
+    DVH_SOS_PLAN(7) DVH_SOS_PLAN(8) DVH_SOS_PLAN(9) DVH_SOS_PLAN(10) DVH_SOS_PLAN(11) DVH_SOS_PLAN(12)
+    DVH_SOS_PLAN(13) DVH_SOS_PLAN(14) DVH_SOS_PLAN(15) DVH_SOS_PLAN(16)
+#undef DVH_SOS_PLAN
+    default: break;
+  }
+  return last_launch();
 }
 
 DVH_API int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t,
@@ -1056,9 +1326,23 @@ DVH_API int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_
   if (n_t <= padlen) return set_error(-4, "The length of the input vector x must be greater than padlen");
   if (padlen < 0 || n_t < 2) return set_error(-2, "invalid padlen / length");
   if (n_rows <= 0) return 0;
-  const SosGeom G = DVH_SOS_MFMA ? sosm_geom(n_rows, row_stride, n_t, padlen) : sos_geom(n_rows, row_stride, n_t, padlen);
-  if (dtype == 0) return sosfiltfilt_dispatch<float>((float*)x, G, sos, n_sec, zi, work, (hipStream_t)stream);
-  if (dtype == 1) return sosfiltfilt_dispatch<double>((double*)x, G, sos, n_sec, zi, work, (hipStream_t)stream);
+  const SosGeom Gm = sosm_geom(n_rows, row_stride, n_t, padlen), Gb = sos_geom(n_rows, row_stride, n_t, padlen);
+  if (dtype == 0) return sosfiltfilt_dispatch<float>((float*)x, Gm, Gb, sos, n_sec, zi, nullptr, work, (hipStream_t)stream);
+  if (dtype == 1) return sosfiltfilt_dispatch<double>((double*)x, Gm, Gb, sos, n_sec, zi, nullptr, work, (hipStream_t)stream);
+  return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
+}
+
+DVH_API int dvh_sosfiltfilt_planned(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t,
+                                    const double* sos, int32_t n_sec, int32_t padlen, const double* zi, const double* plan,
+                                    double* work, void* stream) {
+  if (!x || !sos || !zi || !plan || !work) return set_error(-2, "null pointer argument");
+  if (n_sec <= 0 || n_sec > kMaxSec) return set_error(-4, "unsupported number of second-order sections");
+  if (n_t <= padlen) return set_error(-4, "The length of the input vector x must be greater than padlen");
+  if (padlen < 0 || n_t < 2) return set_error(-2, "invalid padlen / length");
+  if (n_rows <= 0) return 0;
+  const SosGeom Gm = sosm_geom(n_rows, row_stride, n_t, padlen), Gb = sos_geom(n_rows, row_stride, n_t, padlen);
+  if (dtype == 0) return sosfiltfilt_dispatch<float>((float*)x, Gm, Gb, sos, n_sec, zi, plan, work, (hipStream_t)stream);
+  if (dtype == 1) return sosfiltfilt_dispatch<double>((double*)x, Gm, Gb, sos, n_sec, zi, plan, work, (hipStream_t)stream);
   return set_error(-2, "dtype must be 0 (float32) or 1 (float64)");
 }
 

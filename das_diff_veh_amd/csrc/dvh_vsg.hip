@@ -810,23 +810,24 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // max |x| bit pattern over nf4 consecutive float4 (16-byte aligned): unconditional 16-byte buffer
 // loads, kScanDepth per lane in flight (the descriptor's range check zeroes the tail)
+template <int D = kScanDepth>
 __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int nf4, int lane) {
   const __amdgpu_buffer_rsrc_t rs = scan_rsrc(q, (uint32_t)nf4 * 16u);
   const int nsteps = (nf4 + 63) >> 6;
   uint32_t m = 0;
   int off = lane * 16;
-  u32x4 r[kScanDepth];
+  u32x4 r[D];
 #pragma unroll
-  for (int d = 0; d < kScanDepth; ++d) {
+  for (int d = 0; d < D; ++d) {
     r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kScanAux);
     off += 1024;
   }
-  for (int s0 = 0; s0 < nsteps; s0 += kScanDepth) {
+  for (int s0 = 0; s0 < nsteps; s0 += D) {
 #if DVH_SCAN_SLEEP
     __builtin_amdgcn_s_sleep(DVH_SCAN_SLEEP);  // A/B: a throttled stream (64 x N clocks per 16 KB of a wave)
 #endif
 #pragma unroll
-    for (int d = 0; d < kScanDepth; ++d) {
+    for (int d = 0; d < D; ++d) {
       const u32x4 v = r[d] & 0x7fffffffu;
       m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
       r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kScanAux);
@@ -837,13 +838,14 @@ __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int n
 }
 
 // rows [c0, c1) of a window (n_t samples each): max |x| bit pattern over the wave
+template <int D = kScanDepth>
 __device__ __forceinline__ uint32_t scan_rows(const float* __restrict__ base, int64_t ch_stride, int c0, int c1,
                                               int n_t, bool vec, int lane) {
   uint32_t m = 0;
   if (vec && ch_stride == n_t) {  // the unit's rows are one contiguous span
-    m = scan_span(base + (int64_t)c0 * ch_stride, ((c1 - c0) * n_t) >> 2, lane);
+    m = scan_span<D>(base + (int64_t)c0 * ch_stride, ((c1 - c0) * n_t) >> 2, lane);
   } else if (vec) {
-    for (int c = c0; c < c1; ++c) m = max(m, scan_span(base + (int64_t)c * ch_stride, n_t >> 2, lane));
+    for (int c = c0; c < c1; ++c) m = max(m, scan_span<D>(base + (int64_t)c * ch_stride, n_t >> 2, lane));
   } else {
     for (int c = c0; c < c1; ++c)
       for (int t = lane; t < n_t; t += 64) m = max(m, absbits(base[(int64_t)c * ch_stride + t]));
@@ -858,6 +860,7 @@ struct ScanArgs {
 };
 
 // Pull scan units (window, kScanRows channel rows) until none is left; atomicMax into vflag[window].
+template <int D = kScanDepth>
 __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, uint32_t* __restrict__ vflag,
                                            uint32_t* __restrict__ counter, int lane,
                                            const int32_t* __restrict__ sorder = nullptr) {
@@ -871,7 +874,7 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
     const int q = u / upp, c0 = (u - q * upp) * kScanRows;
     const int s = (sorder && !S.tab) ? sld(sorder + q) : q;
     const float* base = S.tab ? A.win + (int64_t)sld(S.tab + s) * A.ch_stride : A.win + (int64_t)s * A.pass_stride;
-    const uint32_t m = scan_rows(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
+    const uint32_t m = scan_rows<D>(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
     if (lane == 0) atomicMax(vflag + s, m);
     u = un;
   }
@@ -1020,7 +1023,7 @@ __device__ __forceinline__ void stack_tasks(E& eng, const VsgArgs& A, const floa
 
 // Persistent validated stack launch: blocks of kFft correlation waves + kScan scan waves (EngF500: two per CU;
 // the 1 024-point engines' LDS and registers allow one).
-template <class E, int kFft, int kScan, int kOcc, bool EXACT = true>
+template <class E, int kFft, int kScan, int kOcc, bool EXACT = true, int kDepth = kScanDepth>
 __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
     const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
@@ -1049,7 +1052,7 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
   // the chunks cover order[0, end of the last chunk): scan in that order when it lists every pass
   const int32_t* sorder = (n_chunk > 0 && sld(chunk_tab + 3 * (n_chunk - 1) + 1) == A.n_pass) ? order : nullptr;
   if (skip) scan_units_skip(A, S, vflag, counter, lane, sorder);
-  else scan_units(A, S, vflag, counter, lane, sorder);
+  else scan_units<kDepth>(A, S, vflag, counter, lane, sorder);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
@@ -1273,6 +1276,15 @@ static int cu_count() {
 #ifndef DVH_VSTACK_OCC
 #define DVH_VSTACK_OCC 4  // EngF500 validated launch: waves per SIMD the registers are sized for (launch bounds)
 #endif
+#ifndef DVH_P1024_FFT
+#define DVH_P1024_FFT 7  // EngP1024 validated launch: correlation waves per block (one block per CU: LDS, registers)
+#endif
+#ifndef DVH_P1024_SCAN
+#define DVH_P1024_SCAN 1  // ... scan waves per block
+#endif
+#ifndef DVH_P1024_DEPTH
+#define DVH_P1024_DEPTH 16  // ... 16-byte loads per lane its scan waves keep in flight (their registers allow more)
+#endif
 #ifndef DVH_PIVOT_TABLE
 #define DVH_PIVOT_TABLE 1  // stack launches at w = 500 with the per-pass pivot-slice spectra table
 #endif
@@ -1284,15 +1296,15 @@ struct VStack {
   int fft, scan, bpc;
   size_t lds;
 };
-template <class E, int F, int SC, int OCC, bool EXACT>
+template <class E, int F, int SC, int OCC, bool EXACT, int DEPTH = kScanDepth>
 static VStack vstack(int bpc) {
-  return VStack{(const void*)vsg_stackv_kernel<E, F, SC, OCC, EXACT>, F, SC, bpc, E::kBlockBytes + F * E::kWaveBytes};
+  return VStack{(const void*)vsg_stackv_kernel<E, F, SC, OCC, EXACT, DEPTH>, F, SC, bpc, E::kBlockBytes + F * E::kWaveBytes};
 }
 static bool get_vstack(int n, VStack* v) {
   switch (n) {
     case 500: *v = vstack<EngF500, DVH_VSTACK_FFT, DVH_VSTACK_SCAN, DVH_VSTACK_OCC, true>(DVH_VSTACK_BPC); return true;
     case 512: *v = vstack<EngStockham<512, true>, 7, 1, 2, false>(1); return true;
-    case 1024: *v = vstack<EngP1024, 7, 1, 2, false>(1); return true;
+    case 1024: *v = vstack<EngP1024, DVH_P1024_FFT, DVH_P1024_SCAN, 2, false, DVH_P1024_DEPTH>(1); return true;
     default: return false;
   }
 }

@@ -183,6 +183,63 @@ constexpr int tw_entries() {
   return SW ? N + (N > 16 ? 4 : 0) + (N > 64 ? 16 : 0) + (N > 256 ? 64 : 0) : N;  // stages Ls < N / 4
 }
 
+// 16-point DFT in registers, natural order in and out (4 x 4: radix-4 DFTs over t2 of a[t1 + 4 t2], twiddles
+// W16^(t1 q2), radix-4 DFTs over t1 into a[q2 + 4 q1]).  HALF: only a[0..7] are non-zero (a zero-padded input).
+template <bool HALF = false>
+__device__ __forceinline__ void dft16(float2 (&a)[16]) {
+  constexpr float c8 = 0.92387953251128675613f, s8 = 0.38268343236508977173f, r2 = 0.70710678118654752440f;
+  float2 y[4][4];
+#pragma unroll
+  for (int t1 = 0; t1 < 4; ++t1) {
+    float2 c[4];
+    if (HALF) {  // DFT4 of (a, b, 0, 0)
+      const float2 u = a[t1], v = a[t1 + 4];
+      c[0] = cadd(u, v);
+      c[1] = add_mi(u, v);
+      c[2] = csub(u, v);
+      c[3] = add_pi(u, v);
+    } else {
+      c[0] = a[t1];
+      c[1] = a[t1 + 4];
+      c[2] = a[t1 + 8];
+      c[3] = a[t1 + 12];
+      Dft<4>::run(c);
+    }
+#pragma unroll
+    for (int q2 = 0; q2 < 4; ++q2) y[t1][q2] = c[q2];
+  }
+  // W16^m, m = t1 q2: 1 (c8, -s8), 2 (r2, -r2), 3 (s8, -c8), 4 (-i), 6 (-r2, -r2), 9 (-c8, s8)
+  y[1][1] = cmul(y[1][1], make_float2(c8, -s8));
+  y[1][2] = cmul(y[1][2], make_float2(r2, -r2));
+  y[1][3] = cmul(y[1][3], make_float2(s8, -c8));
+  y[2][1] = cmul(y[2][1], make_float2(r2, -r2));
+  y[2][2] = mul_mi(y[2][2]);
+  y[2][3] = cmul(y[2][3], make_float2(-r2, -r2));
+  y[3][1] = cmul(y[3][1], make_float2(s8, -c8));
+  y[3][2] = cmul(y[3][2], make_float2(-r2, -r2));
+  y[3][3] = cmul(y[3][3], make_float2(-c8, s8));
+#pragma unroll
+  for (int q2 = 0; q2 < 4; ++q2) {
+    float2 c[4] = {y[0][q2], y[1][q2], y[2][q2], y[3][q2]};
+    Dft<4>::run(c);
+#pragma unroll
+    for (int q1 = 0; q1 < 4; ++q1) a[q2 + 4 * q1] = c[q1];
+  }
+}
+
+// a[t] *= w^t, t = 1..15, from w^1, w^4, w^8 (table reads: every power within three roundings of the table's)
+__device__ __forceinline__ void twiddle16(float2 (&a)[16], float2 w1, float2 w4, float2 w8) {
+  const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+  const float2 lo[4] = {make_float2(1.f, 0.f), w1, w2, w3};
+#pragma unroll
+  for (int t = 1; t < 16; ++t) {
+    const int h = t >> 2, l = t & 3;
+    float2 w = h == 0 ? lo[l] : (h == 1 ? w4 : (h == 2 ? w8 : cmul(w8, w4)));
+    if (h > 0 && l > 0) w = cmul(w, lo[l]);
+    a[t] = cmul(a[t], w);
+  }
+}
+
 template <int N, int Ls, int R, int SW = 0>
 __device__ __forceinline__ void stockham_stage(const float2* __restrict__ in, float2* __restrict__ out,
                                                const float2* __restrict__ tw, int lane) {

@@ -338,7 +338,7 @@ struct FusedOps {
   __device__ FusedOps(char* lds, int wave, int lane_, int w_) : lane(lane_), live_f(false), live_o(false), w(w_) {
     tw = reinterpret_cast<float2*>(lds);
     bufA = reinterpret_cast<float2*>(lds + E::kBlockBytes + (size_t)wave * E::kWaveBytes);
-    bufB = bufA + E::N;
+    bufB = bufA + E::kBufA;
   }
   __device__ __forceinline__ const E& self() const { return *static_cast<const E*>(this); }
 
@@ -714,6 +714,7 @@ struct EngF500 : FusedOps<EngF500, 8, 5> {
   static constexpr int kTabBins = 256;  // bins f <= 250; [255].x: the slice's non-zero flag
   static constexpr size_t kBlockBytes = sizeof(float2) * N;     // twiddle table
   static constexpr size_t kWaveBytes = sizeof(float2) * 2 * N;  // ping-pong buffers
+  static constexpr int kBufA = N;                               // bufB = bufA + kBufA
 
   __device__ EngF500(char* lds, int wave, int lane_) : FusedOps<EngF500, 8, 5>(lds, wave, lane_, N) {}
   static __device__ void block_init(char* lds) { init_twiddles<N>(reinterpret_cast<float2*>(lds)); }
@@ -847,6 +848,9 @@ struct EngF500 : FusedOps<EngF500, 8, 5> {
 // Half-spectrum slots per lane l (each bin f <= 512 exactly once):
 //   j = 0, 1: l, l + 256;  j = 2, 3: 256 - l, 512 - l (lane 0: 128, 384);  j = 4..7: 64 + l, 320 + l, 192 - l,
 //   448 - l;  j = 8: 512 (lane 0 only).
+#ifndef DVH_P1024_R16
+#define DVH_P1024_R16 1  // 1: the transforms as 16 x 16 x 4 (forward) and 4 x 16 x 16 (inverse) radix stages (below)
+#endif
 #ifndef DVH_P1024_SW
 #define DVH_P1024_SW 2  // EngP1024's LDS layout / twiddles (stockham_stage SW bits): 2 = contiguous stage twiddles,
                         // 3 = also the XOR-swizzled layout (conflict-free stores, but its per-store address XORs cost
@@ -865,7 +869,16 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   // twiddle reads; with SW & 1 also conflict-free stage stores: the round-4 build spent 2.9 bank-conflict cycles per
   // LDS instruction on the Ls = 4 stores and the strided twiddle reads)
   static constexpr size_t kBlockBytes = sizeof(float2) * tw_entries<N, SW>();  // twiddle tables
-  static constexpr size_t kWaveBytes = sizeof(float2) * 2 * N;                // ping-pong buffers
+  // Radix-16 form (DVH_P1024_R16): forward = radix 16 (span 1, from the registers, zero-padded half) -> LDS A ->
+  // radix 16 (span 16) -> LDS B -> the paired radix-4 last stage (span 256) in registers; inverse = radix 4 (span 1,
+  // from the registers) -> LDS B -> radix 16 (span 4) -> LDS A -> radix 16 (span 64) -> Y in LDS B.  Two LDS round
+  // trips per transform instead of four, one wave synchronisation per stage boundary, and the twiddle products of two
+  // radix-4 stages merged into one radix-16 stage.  Buffer A is padded (the span-1 forward stage's 16 outputs per lane
+  // at n + n / 16, the span-4 inverse stage's at n + 4 (n / 64)), so the stores and reads of every stage are conflict
+  // free; buffer B is plain.
+  static constexpr bool R16 = DVH_P1024_R16 != 0;
+  static constexpr int kBufA = R16 ? N + N / 16 : N;
+  static constexpr size_t kWaveBytes = sizeof(float2) * (kBufA + N);         // buffers A and B
 
   __device__ EngP1024(char* lds, int wave, int lane_) : FusedOps<EngP1024, 8, 9>(lds, wave, lane_, N / 2) {}
   static __device__ void block_init(char* lds) { init_twiddles<N, SW>(reinterpret_cast<float2*>(lds)); }
@@ -909,6 +922,18 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   }
 
   __device__ __forceinline__ void stage1(const float2 (&z)[8]) const {
+    if constexpr (R16) {
+      // radix-16 butterfly i = lane of x[i + 64 t], t < 16: the prefetched z[t] for t < 8, zero above; outputs
+      // out[16 i + q] at the padded index 17 i + q (16 lanes of a store group: 16 distinct banks)
+      float2 a[16];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) a[t] = z[t];
+      dft16<true>(a);
+      float2* o = bufA + 17 * lane;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) o[q] = a[q];
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = lane + 64 * r;
@@ -916,6 +941,22 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
       // radix-4 DFT of (a0, a1, 0, 0)
       store4(bufB, i, cadd(a0, a1), add_mi(a0, a1), csub(a0, a1), add_pi(a0, a1));
     }
+  }
+
+  // radix-16 Stockham stage (span Ls = 16, 4 or 64) of butterfly i = lane: inputs in[ia(i + 64 t)], twiddles
+  // w^t with w = tw[k N / (16 Ls)] (k = i % Ls), outputs out[oa((i - k) 16 + k + Ls q)]
+  template <int Ls, class IA, class OA>
+  __device__ __forceinline__ void stage16(const float2* in, float2* out, IA ia, OA oa) const {
+    const int i = lane, k = i % Ls;
+    constexpr int TWS = N / (16 * Ls);
+    float2 a[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) a[t] = lds_ld(in, ia(i + 64 * t));
+    twiddle16(a, tw[k * TWS], tw[4 * k * TWS], tw[8 * k * TWS]);
+    dft16<false>(a);
+    const int base = (i - k) * 16 + k;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) out[oa(base + Ls * q)] = a[q];
   }
 
   // radix-4 butterfly k of the last stage (span 256): X[k + 256 q], q < 4
@@ -942,18 +983,25 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   template <class F>
   __device__ __forceinline__ void finish_with(F&& acc) const {
     wave_sync();
-    stockham_stage<N, 4, 4, SW>(bufB, bufA, tw, lane);
-    wave_sync();
-    stockham_stage<N, 16, 4, SW>(bufA, bufB, tw, lane);
-    wave_sync();
-    stockham_stage<N, 64, 4, SW>(bufB, bufA, tw, lane);
+    const float2* src;  // the span-256 stage's input
+    if constexpr (R16) {
+      stage16<16>(bufA, bufB, [](int n) { return n + (n >> 4); }, [](int n) { return n; });
+      src = bufB;
+    } else {
+      stockham_stage<N, 4, 4, SW>(bufB, bufA, tw, lane);
+      wave_sync();
+      stockham_stage<N, 16, 4, SW>(bufA, bufB, tw, lane);
+      wave_sync();
+      stockham_stage<N, 64, 4, SW>(bufB, bufA, tw, lane);
+      src = bufA;
+    }
     wave_sync();
     const int ln = opaque(lane);  // the stage's addresses formed per call, not held in registers between calls
     const bool l0 = ln == 0;
     {
       float2 XA[4], XB[4];
-      last_bfly_from(bufA, ln, XA);
-      last_bfly_from(bufA, l0 ? 128 : 256 - ln, XB);
+      last_bfly_from(src, ln, XA);
+      last_bfly_from(src, l0 ? 128 : 256 - ln, XB);
       acc(0, XA[0], sel(l0, XA[0], XB[3]));
       acc(1, XA[1], sel(l0, XA[3], XB[2]));
       acc(2, XB[0], sel(l0, XB[3], XA[3]));
@@ -962,8 +1010,8 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
     }
     {
       float2 XA[4], XB[4];
-      last_bfly_from(bufA, 64 + ln, XA);
-      last_bfly_from(bufA, 192 - ln, XB);
+      last_bfly_from(src, 64 + ln, XA);
+      last_bfly_from(src, 192 - ln, XB);
       acc(4, XA[0], XB[3]);
       acc(5, XA[1], XB[2]);
       acc(6, XB[0], XA[3]);
@@ -996,6 +1044,13 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
     bfly(l0 ? 128 : 192 - ln, sel(l0, A(2), A(6)), sel(l0, A(3), A(7)), sel(l0, B(3), B(5)), sel(l0, B(2), B(4)));
     bfly(l0 ? 192 : 256 - ln, sel(l0, A(6), A(2)), sel(l0, A(7), A(3)), sel(l0, B(5), B(1)), sel(l0, B(4), B(0)));
     wave_sync();
+    if constexpr (R16) {
+      stage16<4>(bufB, bufA, [](int n) { return n; }, [](int n) { return n + 4 * (n >> 6); });
+      wave_sync();
+      stage16<64>(bufA, bufB, [](int n) { return n + 4 * (n >> 6); }, [](int n) { return n; });
+      wave_sync();
+      return bufB;
+    }
     stockham_stage<N, 4, 4, SW>(bufB, bufA, tw, lane);
     wave_sync();
     stockham_stage<N, 16, 4, SW>(bufA, bufB, tw, lane);

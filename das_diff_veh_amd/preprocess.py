@@ -75,6 +75,21 @@ def _design(dt, flo, fhi, dev):
     return _DESIGNS[key]
 
 
+_PLANS = {}
+
+
+def _plan(key, n_t, sos, padlen, sos_t, zi_t, dev):
+    """dvh_sosfiltfilt_plan's block operators of the design, per record length (formed once; the reference
+    redesigns the same filter for every record)."""
+    k = key + (int(n_t),)
+    if k not in _PLANS:
+        plan = torch.empty(int(_lib.load().dvh_sosfiltfilt_plan_bytes(len(sos))) // 8, dtype=torch.float64, device=dev)
+        _lib.call("dvh_sosfiltfilt_plan", _lib.ptr(sos_t), len(sos), _lib.ptr(zi_t), int(n_t), padlen, _lib.ptr(plan),
+                  _lib.stream_of(dev))
+        _PLANS[k] = plan
+    return _PLANS[k]
+
+
 def bandpass_inplace(data, dt, flo, fhi):
     v = _DeviceView(data)
     t = v.t
@@ -86,8 +101,9 @@ def bandpass_inplace(data, dt, flo, fhi):
         raise ValueError(f"The length of the input vector x must be greater than padlen, which is {padlen}.")
     nbytes = int(_lib.load().dvh_sosfiltfilt_workspace(rows.shape[0], n_t, len(sos), padlen))
     work = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=dev)
-    _lib.call("dvh_sosfiltfilt", _lib.ptr(rows), v.dtype, rows.shape[0], rows.stride(0), n_t, _lib.ptr(sos_t),
-              len(sos), padlen, _lib.ptr(zi_t), _lib.ptr(work), _lib.stream_of(dev))
+    plan = _plan((float(dt), float(flo), float(fhi), str(dev)), n_t, sos, padlen, sos_t, zi_t, dev)
+    _lib.call("dvh_sosfiltfilt_planned", _lib.ptr(rows), v.dtype, rows.shape[0], rows.stride(0), n_t, _lib.ptr(sos_t),
+              len(sos), padlen, _lib.ptr(zi_t), _lib.ptr(plan), _lib.ptr(work), _lib.stream_of(dev))
     v.write_back()
     return data
 

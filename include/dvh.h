@@ -205,6 +205,18 @@ int dvh_ridge(const float* fv, int64_t b_stride, int32_t B, int32_t nV, int32_t 
 int64_t dvh_sosfiltfilt_workspace(int64_t n_rows, int32_t n_t, int32_t n_sec, int32_t padlen);
 int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t, const double* sos,
                     int32_t n_sec, int32_t padlen, const double* zi, double* work, void* stream);
+/* The block operators of dvh_sosfiltfilt's matrix-pipe form (impulse response, zero-input responses, state responses,
+ * the block and group transitions), formed once per filter design and record length n_t (they depend on n_t + 2 padlen
+ * through the scan's group size): plan = device buffer of dvh_sosfiltfilt_plan_bytes(n_sec) bytes.  Then
+ * dvh_sosfiltfilt_planned is dvh_sosfiltfilt without forming them (work: dvh_sosfiltfilt_workspace bytes, as there).
+ * bandpass_data (modules/utils.py:179-189) called once per record of the same shape designs the same filter every
+ * time; the drop-in caches the plan per (design, n_t). */
+int64_t dvh_sosfiltfilt_plan_bytes(int32_t n_sec);
+int dvh_sosfiltfilt_plan(const double* sos, int32_t n_sec, const double* zi, int32_t n_t, int32_t padlen, double* plan,
+                         void* stream);
+int dvh_sosfiltfilt_planned(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t, const double* sos,
+                            int32_t n_sec, int32_t padlen, const double* zi, const double* plan, double* work,
+                            void* stream);
 
 /* SurfaceWaveWindow.mute_along_traj (apis/data_classes.py:49-72): tab[n_pass][n_t][3] =
  * {start, end, taper_start} per time sample; contiguous [n_ch][n_t] per pass. */
