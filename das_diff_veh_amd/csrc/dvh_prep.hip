@@ -1002,19 +1002,35 @@ static int sosm_run(T* x, const SosGeom& G, const double* sos, const double* zi,
   double* Sf = y + G.n_rows * G.n_ext;
   double* Sb = Sf + G.n_rows * G.nb * NST;
   const int Q = sosm_scan_q(G.nb);
-  // persistent-ish grids: at most 2 048 four-wave blocks, each wave looping over tiles
-  auto grid_of = [](int64_t tiles) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, 2048)); };
+  // persistent grids: the blocks that are resident at once (LDS and registers), each wave looping over tiles, so
+  // that every block forms its operator tables once for many tiles
   const int64_t tiles = (G.n_rows * G.nb + 15) / 16;
-  if (G.nb > 1) hipLaunchKernelGGL((sosm_fa_kernel<T, NS>), dim3(grid_of(tiles)), dim3(256), 0, st, (const T*)x, G, plan, Sf);
+  static unsigned res_fa = 0, res_fc = 0, res_bc = 0;
+  auto resident = [](unsigned& cache, const void* fn) {
+    if (!cache) {
+      int n = 0, dev = 0, cus = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 256, 0) != hipSuccess || n <= 0) n = 1;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          cus <= 0)
+        cus = 256;
+      cache = (unsigned)(n * cus);
+    }
+    return cache;
+  };
+  auto grid_of = [](int64_t tiles_, unsigned res) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((tiles_ + 3) / 4, res)); };
+  const unsigned gfa = grid_of(tiles, resident(res_fa, (const void*)sosm_fa_kernel<T, NS>));
+  const unsigned gfc = grid_of(tiles, resident(res_fc, (const void*)sosm_fc_kernel<T, NS>));
+  if (G.nb > 1) hipLaunchKernelGGL((sosm_fa_kernel<T, NS>), dim3(gfa), dim3(256), 0, st, (const T*)x, G, plan, Sf);
   if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, plan, Q, Sf);
-  hipLaunchKernelGGL((sosm_fc_kernel<T, NS>), dim3(grid_of(tiles)), dim3(256), 0, st, (const T*)x, G, plan, zi,
+  hipLaunchKernelGGL((sosm_fc_kernel<T, NS>), dim3(gfc), dim3(256), 0, st, (const T*)x, G, plan, zi,
                      (const double*)Sf, y, Sb);
   hipLaunchKernelGGL((sosm_bf_kernel<T, NS>), dim3((unsigned)((G.n_rows + 63) / 64)), dim3(64), 0, st, x, G, sos, zi,
                      (const double*)y, Sb);
   if (G.nb > 1) {
     if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, plan, Q, Sb);
     const int64_t tb = (G.n_rows * (G.nb - 1) + 15) / 16;
-    hipLaunchKernelGGL((sosm_bc_kernel<T, NS>), dim3(grid_of(tb)), dim3(256), 0, st, x, G, plan, (const double*)y,
+    const unsigned gbc = grid_of(tb, resident(res_bc, (const void*)sosm_bc_kernel<T, NS>));
+    hipLaunchKernelGGL((sosm_bc_kernel<T, NS>), dim3(gbc), dim3(256), 0, st, x, G, plan, (const double*)y,
                        (const double*)Sb);
   }
   const hipError_t e = hipGetLastError();
