@@ -950,11 +950,12 @@ def prep_main(args, world, rank, device):
     bp = float(np.mean([e["bandpass0"].elapsed_time(e["bandpass1"]) for e in evs])) / 1e3
     cl = float(np.mean([e["bandpass1"].elapsed_time(e["cleanup1"]) for e in evs])) / 1e3
     flop = 2.0 * 9 * n_sec * n_ext * n_ch  # sequential sosfiltfilt: forward + backward passes
-    # dvh_sosfiltfilt's block GEMMs on the float64 matrix pipe (csrc/dvh_prep.hip, 32-sample blocks, 16 blocks per
-    # tile): forward end states 2 x 8, forward outputs (lower-triangular Toeplitz + start states) 4 + 8 + 2 x 5,
-    # backward end states 2 x 8, backward outputs 8 + 4 + 2 x 5 v_mfma_f64_16x16x4_f64 per tile (2 NS = 20 states)
-    n_tiles = n_ch * (-(-n_ext // 32)) / 16.0
-    mfma_flop = n_tiles * (16 + 38 + 22) * 2.0 * 16 * 16 * 4
+    # dvh_sosfiltfilt's block GEMMs on the float64 matrix pipe (csrc/dvh_prep.hip, 64-sample blocks, 16 blocks per
+    # tile, 2 NS = 20 states): forward end states 32, forward outputs (lower-triangular Toeplitz with its zero
+    # 16 x 16 tiles skipped, start states) + backward end states 92, backward outputs (upper-triangular) 60
+    # v_mfma_f64_16x16x4_f64 per tile
+    n_tiles = n_ch * (-(-n_ext // 64)) / 16.0
+    mfma_flop = n_tiles * (32 + 92 + 60) * 2.0 * 16 * 16 * 4
     rec_bytes = 4.0 * n_ch * n_t
     # parity (after timing): the step's output against the reference's own path on the whole record
     # (scipy.signal.sosfiltfilt as bandpass_data calls it, then the imputation and norm), and the bandpass
@@ -987,9 +988,9 @@ def prep_main(args, world, rank, device):
                                                           "backward over n_t + 2 padlen (the sequential filter's work)",
                      "mfma_flop_issued": mfma_flop, "mfma_achieved_tflops": mfma_flop / bp / 1e12,
                      "mfma_frac_of_spec": mfma_flop / bp / 1e12 / FP64_MFMA_SPEC_TF,
-                     "mfma_model": "32-sample blocks as float64 MFMA GEMMs: 76 v_mfma_f64_16x16x4_f64 per 16 blocks "
-                                   "(forward end states 16, forward outputs + backward end states 38, backward outputs "
-                                   "22), the state scans between them on the VALU",
+                     "mfma_model": "64-sample blocks as float64 MFMA GEMMs: 184 v_mfma_f64_16x16x4_f64 per 16 blocks "
+                                   "(forward end states 32, forward outputs + backward end states 92, backward outputs "
+                                   "60), the state scans between them on the VALU",
                      "hbm_bytes_model": "record read + y (f64) written and read + record written",
                      "hbm_frac": (2 * rec_bytes + 16.0 * n_ch * n_ext) / bp / 1e9 / HBM_PEAK_GBS},
         "kernels_ms": {"bandpass": bp * 1e3, "trace_cleanup": cl * 1e3},

@@ -534,21 +534,72 @@ __device__ __forceinline__ void sosm_col(const SosmTile& t, int u, int ncpr, int
   }
 }
 
-// forward sequence (odd extension of x) of a tile's columns (blocks of the ext, ncpr = nb)
-template <typename T>
-__device__ __forceinline__ void sosm_load_x(const T* __restrict__ x, const SosGeom& G, const SosmTile& t, int lane,
-                                            double (&v)[16]) {
+// forward sequence (odd extension of x) of a tile's columns (blocks of the ext, ncpr = nb), in two halves so that the
+// loads of the next tile stay in flight under this tile's MFMAs: sosm_fetch_x issues them into registers of x's own
+// type (the samples each lane's sample index reflects to, plus the two reflection centres, x[0] of the last column's
+// row and x[n_t - 1] of the first's), sosm_expand_x forms the extension from them when the tile is consumed.  (A
+// conversion or sum right after a load makes the compiler wait for it there: the prefetch would be a plain load.)
+__device__ __forceinline__ bool sosm_interior(const SosGeom& G, const SosmTile& t) {  // all 16 columns inside x's row
   const int64_t e0 = (int64_t)t.k0 * kSmL;
-  if (t.one_row && e0 >= G.padlen && e0 + 16 * kSmL <= G.padlen + G.n_t) {  // interior: one contiguous run of x
-    const T* p = x + (int64_t)t.r0 * G.row_stride + (e0 - G.padlen) + lane;
+  return t.one_row && e0 >= G.padlen && e0 + 16 * kSmL <= G.padlen + G.n_t;
+}
+template <typename T>
+struct SosmXRaw {
+  T v[16];
+  T xl, xr;
+};
+template <typename T>
+__device__ __forceinline__ void sosm_fetch_x(const T* __restrict__ x, const SosGeom& G, const SosmTile& t, int lane,
+                                             SosmXRaw<T>& raw) {
+  const int nr = (int)G.n_rows;
+  {
+    int rl, kl;
+    sosm_col(t, 15, G.nb, rl, kl);
+    raw.xl = x[(int64_t)min(rl, nr - 1) * G.row_stride];
+    raw.xr = x[(int64_t)min(t.r0, nr - 1) * G.row_stride + G.n_t - 1];
+  }
+  if (sosm_interior(G, t)) {  // one contiguous run of x
+    const T* p = x + (int64_t)t.r0 * G.row_stride + ((int64_t)t.k0 * kSmL - G.padlen) + lane;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = (double)p[64 * u];
+    for (int u = 0; u < 16; ++u) raw.v[u] = p[64 * u];
   } else {
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       int r, k;
       sosm_col(t, u, G.nb, r, k);
-      v[u] = r < G.n_rows ? sosm_ext(x, G, r, (int64_t)k * kSmL + lane) : 0.0;
+      const int64_t j = (int64_t)k * kSmL + lane - G.padlen;
+      int64_t src = j < 0 ? -j : (j < G.n_t ? j : 2 * ((int64_t)G.n_t - 1) - j);
+      src = src < 0 ? 0 : (src >= G.n_t ? G.n_t - 1 : src);  // past the extension: any valid sample (unused)
+      raw.v[u] = x[(int64_t)min(r, nr - 1) * G.row_stride + src];
+    }
+  }
+}
+// the tile's extension samples from its fetched raw values; a column whose reflection centre is not in the raw set
+// (a tile over more than two rows: records of under 16 blocks) reads x directly
+template <typename T>
+__device__ __forceinline__ void sosm_expand_x(const T* __restrict__ x, const SosGeom& G, const SosmTile& t, int lane,
+                                              const SosmXRaw<T>& raw, double (&v)[16]) {
+  if (sosm_interior(G, t)) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = (double)raw.v[u];
+  } else {
+    int rl, kl;
+    sosm_col(t, 15, G.nb, rl, kl);
+    const double xl = (double)raw.xl, xr = (double)raw.xr;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      int r, k;
+      sosm_col(t, u, G.nb, r, k);
+      const int64_t i = (int64_t)k * kSmL + lane, j = i - G.padlen;
+      const double a = (double)raw.v[u];
+      double e;
+      if (j >= 0 && j < G.n_t)
+        e = a;
+      else if (j < 0)
+        e = r == rl ? 2.0 * xl - a : sosm_ext(x, G, r, i);
+      else
+        e = r == t.r0 ? 2.0 * xr - a : sosm_ext(x, G, r, i);
+      v[u] = (r < G.n_rows && i < G.n_ext) ? e : 0.0;
     }
   }
 }
@@ -608,13 +659,26 @@ __global__ __launch_bounds__(256) void sosm_fa_kernel(const T* __restrict__ x, S
   const int nr = (int)G.n_rows;
   const int n_tiles = (nr * G.nb + 15) / 16, stride = gridDim.x * 4;
   int tile = blockIdx.x * 4 + wave;
-  double nx[16];
-  if (tile < n_tiles) sosm_load_x(x, G, sosm_tile(tile, nr, G.nb), lane, nx);
+  // M zi rows m = 16 t + 4 rr + q of this lane (block 0's true end state adds M zi u_0)
+  double mzi[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = 16 * t + 4 * rr + q;
+      mzi[t][rr] = m < NST ? mats[O::Mzi + m] : 0.0;
+    }
+  SosmXRaw<T> raw;
+  if (tile < n_tiles) sosm_fetch_x(x, G, sosm_tile(tile, nr, G.nb), lane, raw);
   for (; tile < n_tiles; tile += stride) {
     const SosmTile tl = sosm_tile(tile, nr, G.nb);
-    wave_barrier_lds();
-    sosm_to_lds(img, lane, nx);
-    if (tile + stride < n_tiles) sosm_load_x(x, G, sosm_tile(tile + stride, nr, G.nb), lane, nx);  // next tile
+    {
+      double v[16];
+      sosm_expand_x(x, G, tl, lane, raw, v);
+      wave_barrier_lds();
+      sosm_to_lds(img, lane, v);
+    }
+    if (tile + stride < n_tiles) sosm_fetch_x(x, G, sosm_tile(tile + stride, nr, G.nb), lane, raw);  // next tile
     wave_barrier_lds();
     doublex4_t acc[2] = {doublex4_t{0.0, 0.0, 0.0, 0.0}, doublex4_t{0.0, 0.0, 0.0, 0.0}};
     const double* bsrc = img + li * kSmLd + q;               // B: sample 4 kk + q of column li
@@ -625,19 +689,14 @@ __global__ __launch_bounds__(256) void sosm_fa_kernel(const T* __restrict__ x, S
 #pragma unroll
       for (int t = 0; t < 2; ++t) acc[t] = mfma_f64x4(asrc[4 * kk * kGaLd + 16 * t], b, acc[t]);
     }
-    // block 0 of a row: its true end state M zi u_0 + E
+    // block 0 of a row: its true end state M zi u_0 + E (u_0: the column's sample 0, in the image)
     int r, k;
     sosm_col(tl, li, G.nb, r, k);
-    const double u0 = (k == 0 && r < nr) ? sosm_ext(x, G, r, 0) : 0.0;
-    if (__ballot(u0 != 0.0) != 0) {
+    const double u0 = (k == 0 && r < nr) ? img[li * kSmLd] : 0.0;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int m = 16 * t + 4 * rr + q;
-          if (m < NST) acc[t][rr] += u0 * mats[O::Mzi + m];
-        }
-    }
+      for (int rr = 0; rr < 4; ++rr) acc[t][rr] += u0 * mzi[t][rr];
     wave_barrier_lds();
     sosm_states_out<NST>(img, lane, acc);
     wave_barrier_lds();
@@ -670,35 +729,49 @@ __global__ __launch_bounds__(256) void sosm_fc_kernel(const T* __restrict__ x, S
   const int nr = (int)G.n_rows;
   const int n_tiles = (nr * G.nb + 15) / 16, stride = gridDim.x * 4;
   int tile = blockIdx.x * 4 + wave;
-  // the start state of column li, states m = KS q + q' (q' < KS) in this lane: contiguous in Sf
+  // the start state of column li, states m = KS q + q' (q' < KS) in this lane: contiguous in Sf (raw loads, block 0's
+  // zi u_0 formed at use, u_0 from the image)
   auto load_s = [&](const SosmTile& t, double (&s)[KS]) {
     int r, k;
     sosm_col(t, li, G.nb, r, k);
-    const bool ok = r < nr;
-    const double u0 = (ok && k == 0) ? sosm_ext(x, G, r, 0) : 0.0;
-    const double* sp = Sf + ((int64_t)r * G.nb + k - 1) * NST;
+    const double* sp = Sf + ((int64_t)min(r, nr - 1) * G.nb + max(k - 1, 0)) * NST;
 #pragma unroll
-    for (int qq = 0; qq < KS; ++qq) {
-      const int m = KS * q + qq;
-      s[qq] = (!ok || m >= NST) ? 0.0 : (k == 0 ? zi[m] * u0 : sp[m]);
-    }
+    for (int qq = 0; qq < KS; ++qq) s[qq] = sp[min(KS * q + qq, NST - 1)];
   };
-  double nx[16], ns[KS];
+  double zim[KS];
+#pragma unroll
+  for (int qq = 0; qq < KS; ++qq) zim[qq] = KS * q + qq < NST ? zi[KS * q + qq] : 0.0;
+  SosmXRaw<T> raw;
+  double ns[KS];
   if (tile < n_tiles) {
     const SosmTile t0 = sosm_tile(tile, nr, G.nb);
-    sosm_load_x(x, G, t0, lane, nx);
+    sosm_fetch_x(x, G, t0, lane, raw);
     load_s(t0, ns);
   }
   for (; tile < n_tiles; tile += stride) {
     const SosmTile tl = sosm_tile(tile, nr, G.nb);
+    {
+      double v[16];
+      sosm_expand_x(x, G, tl, lane, raw, v);
+      wave_barrier_lds();
+      sosm_to_lds(img, lane, v);
+    }
     double sv[KS];
+    {
+      int r, k;
+      sosm_col(tl, li, G.nb, r, k);
+      const bool ok = r < nr;
+      wave_barrier_lds();
+      const double u0 = img[li * kSmLd];
 #pragma unroll
-    for (int qq = 0; qq < KS; ++qq) sv[qq] = ns[qq];
-    wave_barrier_lds();
-    sosm_to_lds(img, lane, nx);
+      for (int qq = 0; qq < KS; ++qq) {
+        const bool real = ok && KS * q + qq < NST;
+        sv[qq] = !real ? 0.0 : (k == 0 ? zim[qq] * u0 : ns[qq]);
+      }
+    }
     if (tile + stride < n_tiles) {  // the next tile's samples and start states, in flight under this tile's MFMAs
       const SosmTile tn = sosm_tile(tile + stride, nr, G.nb);
-      sosm_load_x(x, G, tn, lane, nx);
+      sosm_fetch_x(x, G, tn, lane, raw);
       load_s(tn, ns);
     }
     wave_barrier_lds();
@@ -875,38 +948,47 @@ __global__ __launch_bounds__(256) void sosm_bc_kernel(T* __restrict__ x, SosGeom
 #undef SOSM_B
 
 // The state scan S[k] = S[k] + M S[k - 1], k = 1 .. K - 1 (K = nb - 1 end states; S[0] already true; S[k] holds
-// the zero-state end state E[k] on entry), two-level: one 512-thread block per row, 16 half-waves (lane j = state
-// component j).  The steps are cut into NG <= 16 groups of Q (q covers k in [1 + q Q, 1 + (q + 1) Q)):
+// the zero-state end state E[k] on entry), two-level: one 256-thread block per row, 8 half-waves (lane j = state
+// component j; every row's block resident at once on a 1 024-row record).  The steps are cut into NG <= 8 groups of Q
+// (q covers k in [1 + q Q, 1 + (q + 1) Q)):
 //   1  every group runs the scan from a zero start (group 0 from S[0]): Z[k] = E[k] + M Z[k - 1] (into S[k]);
 //   2  the carries, in order: C_q = Z[last of q] + M^Q C_{q - 1} (C_0 = Z[last of 0], already true);
 //   3  every group q >= 1 adds the carried part: D = M D from D = C_{q - 1}, S[k] = Z[k] + D.
-// 2 Q + NG dependent steps instead of K - 1 (record of 1 024 x 60 s: 46 instead of 235).  A group's operands are
-// loaded kScanPF steps at a time, in one batch ahead of the steps that use them.
-constexpr int kScanHW = 16, kScanPF = 16;
+// 2 Q + NG dependent steps instead of K - 1 (record of 1 024 x 60 s: 68 instead of 235; 16 half-waves per row gave 46
+// steps but two rounds of blocks).  A step is one LDS round trip: the state and the step's own operand come from the
+// LDS in one batch of reads (the 16 steps' operands of a batch are staged there from HBM at once), its result goes
+// to the LDS slot and to HBM by stores nothing waits for.  (Operands held in registers instead left room for two
+// reads in flight: five round trips per step, 43 us per scan.)
+constexpr int kScanHW = 8, kScanPF = 16;
 __host__ __device__ constexpr int sosm_scan_q(int nb) { return nb > 2 ? (nb - 2 + kScanHW - 1) / kScanHW : 1; }
 
 template <int NS>
-__global__ __launch_bounds__(512) void sosm_scan_kernel(SosGeom G, const double* __restrict__ mats, int32_t Q,
+__global__ __launch_bounds__(32 * kScanHW, 4) void sosm_scan_kernel(SosGeom G, const double* __restrict__ mats, int32_t Q,
                                                         double* __restrict__ S) {
   using O = SosmMats<NS>;
   constexpr int NST = 2 * NS;
   __shared__ __attribute__((aligned(16))) double sv[kScanHW][32];
-  __shared__ double carry[kScanHW][NST], zlast[kScanHW][NST], mqs[NST * NST];
+  __shared__ double zb[kScanHW][kScanPF][NST];  // the batch's operands, then its results
+  __shared__ double carry[kScanHW][NST], zlast[kScanHW][NST];
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   const bool act = j < NST;
+  const int jc = act ? j : 0;
   double* Sr = S + (int64_t)blockIdx.x * G.nb * NST;
   const int K = G.nb - 1;
   const int k0 = 1 + hw * Q, k1 = min(1 + (hw + 1) * Q, K);  // this half-wave's group [k0, k1)
   const int ng = K > 1 ? (K - 1 + Q - 1) / Q : 0;              // non-empty groups
-  auto matvec = [&](const double* A, double add) {  // add + sum_i A[i] x_i (row j of the matrix), x from the LDS slot
+  // add + sum_i A[i] x_i (row j of the matrix), x from the LDS slot: every read of the step issued together
+  auto matvec = [&](const double* A, double add) {
     wave_barrier_lds();
     const double2* v2 = reinterpret_cast<const double2*>(sv[hw]);
+    double2 u[NST / 2];
+#pragma unroll
+    for (int i = 0; i < NST / 2; ++i) u[i] = v2[i];
     double pa[4] = {add, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int i = 0; i < NST / 2; ++i) {
-      const double2 u = v2[i];
-      pa[(2 * i) & 3] += A[2 * i] * u.x;
-      pa[(2 * i + 1) & 3] += A[2 * i + 1] * u.y;
+      pa[(2 * i) & 3] += A[2 * i] * u[i].x;
+      pa[(2 * i + 1) & 3] += A[2 * i + 1] * u[i].y;
     }
     return (pa[0] + pa[1]) + (pa[2] + pa[3]);
   };
@@ -916,57 +998,186 @@ __global__ __launch_bounds__(512) void sosm_scan_kernel(SosGeom G, const double*
   };
   double m[NST];
 #pragma unroll
-  for (int i = 0; i < NST; ++i) m[i] = act ? mats[O::M + j * NST + i] : 0.0;
-  // level 1: zero-start scans of the groups (group 0 from the true S[0])
-  put((hw == 0 && act) ? Sr[j] : 0.0);
-  double cur[kScanPF];
-  for (int kb = k0; kb < k0 + Q; kb += kScanPF) {
+  for (int i = 0; i < NST; ++i) {
+    const double v = mats[O::M + jc * NST + i];
+    m[i] = act ? v : 0.0;
+  }
+  // rows kb .. kb + 15 of this group into zb[hw] (zeros past the group; loads unconditional, clamped, so that the
+  // compiler issues them together instead of one under each lane test)
+  auto stage = [&](int kb) {
+    double v[kScanPF];
 #pragma unroll
-    for (int t = 0; t < kScanPF; ++t) cur[t] = (act && kb + t < k1) ? Sr[(int64_t)(kb + t) * NST + j] : 0.0;
+    for (int t = 0; t < kScanPF; ++t) v[t] = Sr[(int64_t)min(kb + t, K - 1) * NST + jc];
+#pragma unroll
+    for (int t = 0; t < kScanPF; ++t)
+      if (act) zb[hw][t][j] = kb + t < k1 ? v[t] : 0.0;
+  };
+  // level 1: zero-start scans of the groups (group 0 from the true S[0]); every half-wave runs Q steps rounded up to
+  // whole batches (steps past the group compute on zeros or run on past its end, and store nothing)
+  {
+    const double s0 = Sr[jc];
+    put((hw == 0 && act) ? s0 : 0.0);
+  }
+  double zl = 0.0;
+  for (int kb = k0; kb < k0 + Q; kb += kScanPF) {
+    stage(kb);
 #pragma unroll
     for (int t = 0; t < kScanPF; ++t) {
-      const int k = kb + t;
-      if (k < k0 + Q) {  // every half-wave runs Q steps (lanes past their group compute on zeros, store nothing)
-        const double z = matvec(m, cur[t]);
-        if (act && k < k1) Sr[(int64_t)k * NST + j] = z;
-        if (act && k == k1 - 1) zlast[hw][j] = z;  // the group's last Z, for the carries
-        cur[t] = z;
-        put(z);
-      }
+      const double z = matvec(m, act ? zb[hw][t][j] : 0.0);
+      zl = kb + t == k1 - 1 ? z : zl;  // the group's last Z, for the carries
+      put(z);
+      if (act) zb[hw][t][j] = z;
+      if (act && kb + t < k1) Sr[(int64_t)(kb + t) * NST + j] = z;
     }
   }
-  for (int v = threadIdx.x; v < NST * NST; v += blockDim.x) mqs[v] = mats[O::MQ + v];
+  if (act) zlast[hw][j] = zl;
   __syncthreads();
-  // level 2: carries by one half-wave
+  // level 2: carries by one half-wave (M^Q rows from HBM: six steps)
   if (hw == 0) {
+    double mq[NST];
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const double v = mats[O::MQ + jc * NST + i];
+      mq[i] = act ? v : 0.0;
+    }
     double c = act ? zlast[0][j] : 0.0;
     if (act) carry[0][j] = c;
     for (int g = 1; g + 1 < ng; ++g) {
       put(c);
-      c = matvec(mqs + (act ? j : 0) * NST, act ? zlast[g][j] : 0.0);
+      c = matvec(mq, act ? zlast[g][j] : 0.0);
       if (act) carry[g][j] = c;
     }
   }
   __syncthreads();
-  // level 3: the carried part of groups q >= 1 (Z from the registers when the group fits one batch)
+  // level 3: the carried part of groups q >= 1 (Z from the LDS when the group fits one batch, else from HBM again)
   if (hw >= 1 && hw < ng) {
     double d = act ? carry[hw - 1][j] : 0.0;
     for (int kb = k0; kb < k1; kb += kScanPF) {
-      if (Q > kScanPF) {
-#pragma unroll
-        for (int t = 0; t < kScanPF; ++t) cur[t] = (act && kb + t < k1) ? Sr[(int64_t)(kb + t) * NST + j] : 0.0;
-      }
+      if (Q > kScanPF) stage(kb);
 #pragma unroll
       for (int t = 0; t < kScanPF; ++t) {
-        const int k = kb + t;
-        if (k < k1) {
-          put(d);
-          d = matvec(m, 0.0);
-          if (act) Sr[(int64_t)k * NST + j] = cur[t] + d;
-        }
+        put(d);
+        d = matvec(m, 0.0);
+        if (act && kb + t < k1) Sr[(int64_t)(kb + t) * NST + j] = zb[hw][t][j] + d;
       }
     }
   }
+}
+
+// The same scan with the row's states resident in the LDS (records of up to kScanCap / NST end states: 240 blocks of
+// 64 samples at NS = 10, 61 s at 250 Hz): the row's E[0 .. K) come in by one coalesced batch of 16-byte loads, level 1
+// turns them into Z in place, level 3 stores S = Z + D straight from there.  HBM sees each state read once and written
+// once (the staged kernel above reads E, writes Z, reads Z again and writes S: twice the bytes, in bursts that no
+// step overlaps).
+constexpr int kScanCap = 4800;  // doubles: 37.5 KB, with the carries and the broadcast slots 40 KB (4 rows per CU)
+template <int NS>
+__global__ __launch_bounds__(32 * kScanHW, 4) void sosm_scanr_kernel(SosGeom G, const double* __restrict__ mats,
+                                                                    int32_t Q, double* __restrict__ S) {
+  using O = SosmMats<NS>;
+  constexpr int NST = 2 * NS;
+  __shared__ __attribute__((aligned(16))) double zf[kScanCap];
+  __shared__ __attribute__((aligned(16))) double sv[kScanHW][NST + (NST & 1)];
+  __shared__ double carry[kScanHW][NST];
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const bool act = j < NST;
+  const int jc = act ? j : 0;
+  double* Sr = S + (int64_t)blockIdx.x * G.nb * NST;
+  const int K = G.nb - 1;
+  const int k0 = 1 + hw * Q, k1 = min(1 + (hw + 1) * Q, K);  // this half-wave's group [k0, k1)
+  const int ng = K > 1 ? (K - 1 + Q - 1) / Q : 0;              // non-empty groups
+  double m[NST];
+#pragma unroll
+  for (int i = 0; i < NST; ++i) {
+    const double v = mats[O::M + jc * NST + i];
+    m[i] = act ? v : 0.0;
+  }
+  // E[0 .. K) -> zf: K NST doubles by LDS-DMA (16 bytes per lane, no registers: M stays in them)
+  {
+    const int n16 = K * NST / 2;  // NST even
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int c = 0; c * 32 * kScanHW < n16; ++c) {
+      const int e0 = c * 32 * kScanHW + w * 64, e = e0 + lane;
+      if (e < n16)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(Sr + 2 * e),
+                                         (__attribute__((address_space(3))) void*)(zf + 2 * e0), 16, 0, 0);
+    }
+  }
+  __syncthreads();
+  // add + sum_i A[i] x_i, x = the NST doubles at xs (LDS, broadcast): every read of the step issued together
+  auto matvec = [&](const double* A, const double* xs, double add) {
+    const double2* v2 = reinterpret_cast<const double2*>(xs);
+    double2 u[NST / 2];
+#pragma unroll
+    for (int i = 0; i < NST / 2; ++i) u[i] = v2[i];
+    double pa[4] = {add, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < NST / 2; ++i) {
+      pa[(2 * i) & 3] += A[2 * i] * u[i].x;
+      pa[(2 * i + 1) & 3] += A[2 * i + 1] * u[i].y;
+    }
+    return (pa[0] + pa[1]) + (pa[2] + pa[3]);
+  };
+  // level 1: Z[k] = E[k] + M Z[k - 1] in place (group 0 from the true S[0]; the others from zero: their first step
+  // takes E alone, the product with the neighbouring group's row discarded)
+#pragma unroll 1
+  for (int k = k0; k < k1; ++k) {
+    wave_barrier_lds();
+    const double z = matvec(m, zf + (k - 1) * NST, zf[k * NST + jc]);
+    const double e = zf[k * NST + jc];
+    wave_barrier_lds();
+    if (act) zf[k * NST + j] = (k == k0 && hw > 0) ? e : z;
+  }
+  __syncthreads();
+  // level 2: the carries C_g (true state at the end of group g), in order, by one half-wave
+  if (hw == 0) {
+    double mq[NST];
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const double v = mats[O::MQ + jc * NST + i];
+      mq[i] = act ? v : 0.0;
+    }
+    double c = act ? zf[(min(1 + Q, K) - 1) * NST + j] : 0.0;
+    if (act) carry[0][j] = c;
+#pragma unroll 1
+    for (int g = 1; g + 1 < ng; ++g) {
+      if (act) sv[0][j] = c;
+      wave_barrier_lds();
+      c = matvec(mq, sv[0], act ? zf[(min(1 + (g + 1) * Q, K) - 1) * NST + j] : 0.0);
+      wave_barrier_lds();
+      if (act) carry[g][j] = c;
+    }
+  }
+  __syncthreads();
+  // level 3: S[k] = Z[k] + M^(k - k0 + 1) C_(q - 1) for groups q >= 1, S[k] = Z[k] for group 0, stored to HBM (M
+  // again from memory, L2-resident: holding it over level 2 beside M^Q would spill; the pointer is laundered so that
+  // the compiler does not reuse the first loads' registers instead)
+  const double* mats3 = mats;
+  asm volatile("" : "+s"(mats3));
+#pragma unroll
+  for (int i = 0; i < NST; ++i) {
+    const double v = mats3[O::M + jc * NST + i];
+    m[i] = act ? v : 0.0;
+  }
+  double d = (hw >= 1 && hw < ng && act) ? carry[hw - 1][j] : 0.0;
+#pragma unroll 1
+  for (int k = k0; k < k1; ++k) {
+    if (hw >= 1) {
+      if (act) sv[hw][j] = d;
+      wave_barrier_lds();
+      d = matvec(m, sv[hw], 0.0);
+      wave_barrier_lds();
+    }
+    if (act) Sr[(int64_t)k * NST + j] = zf[k * NST + j] + d;
+  }
+}
+
+template <int NS>
+static void sosm_scan(const SosGeom& G, const double* plan, int Q, double* S, hipStream_t st) {
+  if (G.nb <= 2) return;
+  if ((int64_t)(G.nb - 1) * 2 * NS <= kScanCap)
+    hipLaunchKernelGGL(sosm_scanr_kernel<NS>, dim3((unsigned)G.n_rows), dim3(32 * kScanHW), 0, st, G, plan, Q, S);
+  else
+    hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(32 * kScanHW), 0, st, G, plan, Q, S);
 }
 
 static SosGeom sosm_geom(int64_t n_rows, int64_t row_stride, int32_t n_t, int32_t padlen) {
@@ -1021,13 +1232,13 @@ static int sosm_run(T* x, const SosGeom& G, const double* sos, const double* zi,
   const unsigned gfa = grid_of(tiles, resident(res_fa, (const void*)sosm_fa_kernel<T, NS>));
   const unsigned gfc = grid_of(tiles, resident(res_fc, (const void*)sosm_fc_kernel<T, NS>));
   if (G.nb > 1) hipLaunchKernelGGL((sosm_fa_kernel<T, NS>), dim3(gfa), dim3(256), 0, st, (const T*)x, G, plan, Sf);
-  if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, plan, Q, Sf);
+  sosm_scan<NS>(G, plan, Q, Sf, st);
   hipLaunchKernelGGL((sosm_fc_kernel<T, NS>), dim3(gfc), dim3(256), 0, st, (const T*)x, G, plan, zi,
                      (const double*)Sf, y, Sb);
   hipLaunchKernelGGL((sosm_bf_kernel<T, NS>), dim3((unsigned)((G.n_rows + 63) / 64)), dim3(64), 0, st, x, G, sos, zi,
                      (const double*)y, Sb);
   if (G.nb > 1) {
-    if (G.nb > 2) hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(512), 0, st, G, plan, Q, Sb);
+    sosm_scan<NS>(G, plan, Q, Sb, st);
     const int64_t tb = (G.n_rows * (G.nb - 1) + 15) / 16;
     const unsigned gbc = grid_of(tb, resident(res_bc, (const void*)sosm_bc_kernel<T, NS>));
     hipLaunchKernelGGL((sosm_bc_kernel<T, NS>), dim3(gbc), dim3(256), 0, st, x, G, plan, (const double*)y,
