@@ -607,6 +607,12 @@ __device__ __forceinline__ void sosm_expand_x(const T* __restrict__ x, const Sos
 // forward output y of a tile's columns (ncpr = nb - 1: blocks k < nb - 1 of each row, all full)
 __device__ __forceinline__ void sosm_load_y(const double* __restrict__ y, const SosGeom& G, const SosmTile& t, int lane,
                                             double (&v)[16]) {
+  if (t.one_row) {  // one contiguous run of the row's y (every column a full block)
+    const double* p = y + (int64_t)t.r0 * G.n_ext + (int64_t)t.k0 * kSmL + lane;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = p[64 * u];
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     int r, k;
@@ -701,13 +707,22 @@ __global__ __launch_bounds__(256) void sosm_fa_kernel(const T* __restrict__ x, S
     sosm_states_out<NST>(img, lane, acc);
     wave_barrier_lds();
     // 16 x NST states, element v = column * NST + m; only full blocks (k < nb - 1) keep an end state
+    if (tl.one_row && tl.k0 + 16 <= G.nb - 1) {  // one contiguous run of Sf
+      double* sp = Sf + ((int64_t)tl.r0 * G.nb + tl.k0) * NST;
 #pragma unroll
-    for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
-      const int v = lane + 64 * u;
-      if (v < 16 * NST) {
-        int rc, kc;
-        sosm_col(tl, v / NST, G.nb, rc, kc);
-        if (rc < nr && kc < G.nb - 1) Sf[((int64_t)rc * G.nb + kc) * NST + v % NST] = img[v];
+      for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
+        const int v = lane + 64 * u;
+        if (v < 16 * NST) sp[v] = img[v];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
+        const int v = lane + 64 * u;
+        if (v < 16 * NST) {
+          int rc, kc;
+          sosm_col(tl, v / NST, G.nb, rc, kc);
+          if (rc < nr && kc < G.nb - 1) Sf[((int64_t)rc * G.nb + kc) * NST + v % NST] = img[v];
+        }
       }
     }
   }
@@ -804,24 +819,40 @@ __global__ __launch_bounds__(256) void sosm_fc_kernel(const T* __restrict__ x, S
     wave_barrier_lds();
     sosm_acc_to_lds(img, lane, acc);
     wave_barrier_lds();
+    const bool full = tl.one_row && tl.k0 + 16 <= G.nb - 1;  // 16 full blocks of one row: plain runs
+    if (full) {
+      double* yp = y + (int64_t)tl.r0 * G.n_ext + (int64_t)tl.k0 * kSmL + lane;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      int r, k;
-      sosm_col(tl, u, G.nb, r, k);
-      const int64_t i = (int64_t)k * kSmL + lane;
-      if (r < nr && i < G.n_ext) y[(int64_t)r * G.n_ext + i] = img[u * kSmLd + lane];
+      for (int u = 0; u < 16; ++u) yp[64 * u] = img[u * kSmLd + lane];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        int r, k;
+        sosm_col(tl, u, G.nb, r, k);
+        const int64_t i = (int64_t)k * kSmL + lane;
+        if (r < nr && i < G.n_ext) y[(int64_t)r * G.n_ext + i] = img[u * kSmLd + lane];
+      }
     }
     // E_b of full blocks at backward index nb - 1 - k
     wave_barrier_lds();
     sosm_states_out<NST>(img, lane, e);
     wave_barrier_lds();
+    if (full) {  // column c at backward index nb - 1 - k0 - c: descending runs of NST
+      double* sp = Sb + ((int64_t)tl.r0 * G.nb + (G.nb - 1 - tl.k0)) * NST;
 #pragma unroll
-    for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
-      const int v = lane + 64 * u;
-      if (v < 16 * NST) {
-        int rc, kc;
-        sosm_col(tl, v / NST, G.nb, rc, kc);
-        if (rc < nr && kc < G.nb - 1) Sb[((int64_t)rc * G.nb + (G.nb - 1 - kc)) * NST + v % NST] = img[v];
+      for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
+        const int v = lane + 64 * u;
+        if (v < 16 * NST) sp[v % NST - (v / NST) * NST] = img[v];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
+        const int v = lane + 64 * u;
+        if (v < 16 * NST) {
+          int rc, kc;
+          sosm_col(tl, v / NST, G.nb, rc, kc);
+          if (rc < nr && kc < G.nb - 1) Sb[((int64_t)rc * G.nb + (G.nb - 1 - kc)) * NST + v % NST] = img[v];
+        }
       }
     }
   }
@@ -936,12 +967,19 @@ __global__ __launch_bounds__(256) void sosm_bc_kernel(T* __restrict__ x, SosGeom
     sosm_acc_to_lds(img, lane, acc);
     wave_barrier_lds();
     // v at ext index k L + i -> x[j = k L + i - padlen] when 0 <= j < n_t
+    const int64_t j0 = (int64_t)tl.k0 * kSmL - G.padlen;
+    if (tl.one_row && j0 >= 0 && j0 + 16 * kSmL <= G.n_t) {  // one contiguous run of x
+      T* xp = x + (int64_t)tl.r0 * G.row_stride + j0 + lane;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      int r, k;
-      sosm_col(tl, u, nc, r, k);
-      const int64_t j = (int64_t)k * kSmL + lane - G.padlen;
-      if (r < nr && j >= 0 && j < G.n_t) x[(int64_t)r * G.row_stride + j] = (T)img[u * kSmLd + lane];
+      for (int u = 0; u < 16; ++u) xp[64 * u] = (T)img[u * kSmLd + lane];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        int r, k;
+        sosm_col(tl, u, nc, r, k);
+        const int64_t j = (int64_t)k * kSmL + lane - G.padlen;
+        if (r < nr && j >= 0 && j < G.n_t) x[(int64_t)r * G.row_stride + j] = (T)img[u * kSmLd + lane];
+      }
     }
   }
 }

@@ -22,7 +22,7 @@ for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
     for row in csv.DictReader(open(f)):
         if filt not in row["Kernel_Name"]:
             continue
-        k = row["Kernel_Name"].split("(")[0].split()[-1][:60]
+        k = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("dvh::", "")[:60]
         per[k][row["Counter_Name"]][(f, row["Dispatch_Id"])] += float(row["Counter_Value"])
 res = {k: {c: sum(v.values()) / len(v) for c, v in cs.items()} for k, cs in per.items()}
 json.dump(res, open(d + ".json", "w"), indent=1)
