@@ -748,8 +748,8 @@ def pmc_lookup(kernel, layout, key):
     launch layout equals this run's.  (None, note) when no summary matches: counters of a different
     launch shape divided by this run's launch time would be wrong by the ratio of the shapes."""
     sfx = "" if layout["workload"] == "synth10k" else "_" + layout["workload"]
-    if "w" in layout and layout["workload"] == "synth10k":
-        sfx = f"_w{layout['w']}"  # tools/pmc.sh <tag> w499
+    if "w" in layout:  # tools/pmc.sh <tag> w499 | weights_w499
+        sfx = f"_w{layout['w']}" if layout["workload"] == "synth10k" else f"{sfx}_w{layout['w']}"
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_summary{sfx}.json")), reverse=True):
         try:
             d = json.load(open(f))

@@ -70,8 +70,12 @@ case $mode in
   final)
     tag=$1
     run_tests || exit 1
-    for wl in synth10k sliding weights w499; do
+    for wl in synth10k sliding weights w499 weights_w499; do
       bash "$0" pmc $tag $wl || exit 1
+    done
+    for o in fused corr7 corr; do  # weights: the SQ breakdown of the launch, the correlation alone, the plain kernel
+      EXP_ARGS="--workload weights" timeout -k 10 400 bash tools/pmc_exp.sh ${tag}w_$o $o > gpurun_out/pmcx_${tag}w_$o.log 2>&1 \
+        || { echo pmcx $o failed; tail -3 gpurun_out/pmcx_${tag}w_$o.log; exit 1; }
     done
     bash tools/pmc_timelapse.sh $tag > gpurun_out/pmc_tl.log 2>&1 || { echo pmc tl failed; tail -5 gpurun_out/pmc_tl.log; exit 1; }
     rm -rf gpurun_out/pmc_${tag}* ;;
@@ -82,6 +86,7 @@ case $mode in
     bench_line gpurun_out/${tag}_bench_sliding.json --workload sliding --steps 4 --warmup 1 || exit 1
     bench_line gpurun_out/${tag}_bench_timelapse.json --workload timelapse || exit 1
     bench_line gpurun_out/${tag}_bench_w499.json --w499 || exit 1
+    bench_line gpurun_out/${tag}_bench_weights_w499.json --workload weights --w499 || exit 1
     bench_line gpurun_out/${tag}_bench_prep.json --workload prep --steps 20 --warmup 3 || exit 1
     bench_line gpurun_out/${tag}_bench_bootstrap.json --workload bootstrap --steps 5 --warmup 1 || exit 1
     bench_line gpurun_out/${tag}_bench_speeds_host.json --workload speeds-host --steps 3 --warmup 1 || exit 1

@@ -9,6 +9,7 @@ tag=${1:-r1}
 wl=${2:-synth10k}
 sfx=""; [ "$wl" = synth10k ] || sfx="_$wl"
 bargs="--workload $wl"; [ "$wl" = w499 ] && bargs="--workload synth10k --w499"  # synth10k at w = 499
+[ "$wl" = weights_w499 ] && bargs="--workload weights --w499"  # configs[1] at w = 499
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/pmc_$tag$sfx
 [ -x tools/calib/fetch_calib ] || { echo "build tools/calib/fetch_calib first"; exit 1; }
