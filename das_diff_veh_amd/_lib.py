@@ -44,6 +44,7 @@ SIGNATURES = {
     "dvh_sosfiltfilt_workspace": [_i64, _i32, _i32, _i32],
     "dvh_sosfiltfilt": [_p, _i32, _i64, _i64, _i32, _p, _i32, _i32, _p, _p, _p],
     "dvh_sosfiltfilt_plan_bytes": [_i32],
+    "dvh_sos_pole_radius": [_p, _i32],
     "dvh_sosfiltfilt_plan": [_p, _i32, _p, _i32, _i32, _p, _p],
     "dvh_sosfiltfilt_planned": [_p, _i32, _i64, _i64, _i32, _p, _i32, _i32, _p, _p, _p, _p],
     "dvh_trace_cleanup": [_p, _i32, _i64, _i64, _i32, _i32, _f64, _p, _p, _p],
@@ -52,7 +53,7 @@ SIGNATURES = {
     "dvh_mute_time": [_p, _i32, _i64, _i32, _p, _p],
 }
 _RESTYPES = {"dvh_last_error": C.c_char_p, "dvh_vsg_stack_workspace": C.c_int64, "dvh_sosfiltfilt_workspace": C.c_int64,
-             "dvh_sosfiltfilt_plan_bytes": C.c_int64}
+             "dvh_sosfiltfilt_plan_bytes": C.c_int64, "dvh_sos_pole_radius": C.c_double}
 
 _lock = threading.Lock()
 _lib = None

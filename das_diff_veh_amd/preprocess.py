@@ -76,13 +76,19 @@ def _design(dt, flo, fhi, dev):
 
 
 _PLANS = {}
+SOS_MFMA_MAX_POLE = 0.999  # include/dvh.h DVH_SOS_MFMA_MAX_POLE
 
 
 def _plan(key, n_t, sos, padlen, sos_t, zi_t, dev):
     """dvh_sosfiltfilt_plan's block operators of the design, per record length (formed once; the reference
-    redesigns the same filter for every record)."""
+    redesigns the same filter for every record); None (the block recursion) for a design whose largest pole
+    radius exceeds SOS_MFMA_MAX_POLE, where the matrix form's rounding would pass 1e-10 of the output."""
     k = key + (int(n_t),)
     if k not in _PLANS:
+        s64 = np.ascontiguousarray(sos, dtype=np.float64)
+        if _lib.load().dvh_sos_pole_radius(s64.ctypes.data, len(sos)) > SOS_MFMA_MAX_POLE:
+            _PLANS[k] = None
+            return None
         plan = torch.empty(int(_lib.load().dvh_sosfiltfilt_plan_bytes(len(sos))) // 8, dtype=torch.float64, device=dev)
         _lib.call("dvh_sosfiltfilt_plan", _lib.ptr(sos_t), len(sos), _lib.ptr(zi_t), int(n_t), padlen, _lib.ptr(plan),
                   _lib.stream_of(dev))
@@ -103,7 +109,8 @@ def bandpass_inplace(data, dt, flo, fhi):
     work = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=dev)
     plan = _plan((float(dt), float(flo), float(fhi), str(dev)), n_t, sos, padlen, sos_t, zi_t, dev)
     _lib.call("dvh_sosfiltfilt_planned", _lib.ptr(rows), v.dtype, rows.shape[0], rows.stride(0), n_t, _lib.ptr(sos_t),
-              len(sos), padlen, _lib.ptr(zi_t), _lib.ptr(plan), _lib.ptr(work), _lib.stream_of(dev))
+              len(sos), padlen, _lib.ptr(zi_t), None if plan is None else _lib.ptr(plan), _lib.ptr(work),
+              _lib.stream_of(dev))
     v.write_back()
     return data
 

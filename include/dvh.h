@@ -200,17 +200,22 @@ int dvh_ridge(const float* fv, int64_t b_stride, int32_t B, int32_t nV, int32_t 
 
 /* scipy.signal.sosfiltfilt(sos, x, axis=-1) per row (bandpass_data, modules/utils.py:179-189);
  * zi = sosfilt_zi(sos) [n_sec][2] (device); n_sec <= 16.  Time-parallel: each row is filtered in blocks
- * (zero-state block filters, a scan of the 2 n_sec block states, re-filter), forward then backward.
- * work: device buffer of dvh_sosfiltfilt_workspace(n_rows, n_t, n_sec, padlen) bytes. */
+ * (zero-state block filters, a scan of the 2 n_sec block states, re-filter), forward then backward, the blocks by
+ * the filter's own recursion (any stable design).  work: device buffer of dvh_sosfiltfilt_workspace(n_rows, n_t,
+ * n_sec, padlen) bytes. */
 int64_t dvh_sosfiltfilt_workspace(int64_t n_rows, int32_t n_t, int32_t n_sec, int32_t padlen);
 int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t, const double* sos,
                     int32_t n_sec, int32_t padlen, const double* zi, double* work, void* stream);
-/* The block operators of dvh_sosfiltfilt's matrix-pipe form (impulse response, zero-input responses, state responses,
- * the block and group transitions), formed once per filter design and record length n_t (they depend on n_t + 2 padlen
- * through the scan's group size): plan = device buffer of dvh_sosfiltfilt_plan_bytes(n_sec) bytes.  Then
- * dvh_sosfiltfilt_planned is dvh_sosfiltfilt without forming them (work: dvh_sosfiltfilt_workspace bytes, as there).
+/* The matrix-pipe form: the blocks as float64 MFMA GEMMs with the block operators (impulse response, zero-input
+ * responses, state responses, the block and group transitions), formed once per filter design and record length n_t
+ * (they depend on n_t + 2 padlen through the scan's group size): plan = device buffer of dvh_sosfiltfilt_plan_bytes(
+ * n_sec) bytes.  dvh_sosfiltfilt_planned filters with them (work: dvh_sosfiltfilt_workspace bytes; plan NULL: the
+ * recursion, as dvh_sosfiltfilt).  Its rounding grows with the largest pole radius r (host sos: dvh_sos_pole_radius):
+ * 1e-13 relative at r = 0.9956, 5e-10 at r = 0.99973, so plan it only for r <= DVH_SOS_MFMA_MAX_POLE.
  * bandpass_data (modules/utils.py:179-189) called once per record of the same shape designs the same filter every
  * time; the drop-in caches the plan per (design, n_t). */
+#define DVH_SOS_MFMA_MAX_POLE 0.999
+double dvh_sos_pole_radius(const double* sos_host, int32_t n_sec);
 int64_t dvh_sosfiltfilt_plan_bytes(int32_t n_sec);
 int dvh_sosfiltfilt_plan(const double* sos, int32_t n_sec, const double* zi, int32_t n_t, int32_t padlen, double* plan,
                          void* stream);

@@ -577,3 +577,16 @@ def test_switch_interval_is_opt_in_and_refcounted(monkeypatch):
     go.set()
     th.join()
     assert sys.getswitchinterval() == prev
+
+
+def test_sos_pole_radius_matches_numpy_roots():
+    """dvh_sos_pole_radius (host arithmetic, no GPU): the largest |pole| of a design's sections, the quantity that
+    picks sosfiltfilt's matrix-pipe form (include/dvh.h DVH_SOS_MFMA_MAX_POLE)."""
+    from das_diff_veh_amd import _lib
+    from das_diff_veh_amd.preprocess import butter_bandpass_sos
+    for dt, flo, fhi in ((0.004, 1.2, 30), (0.004, 0.08, 1), (0.002, 1, 30), (0.004, 5, 60)):
+        sos = np.ascontiguousarray(butter_bandpass_sos(dt, flo, fhi), dtype=np.float64)
+        ref = max(np.abs(np.roots(s[3:])).max() for s in sos)
+        got = _lib.load().dvh_sos_pole_radius(sos.ctypes.data, len(sos))
+        assert abs(got - ref) < 1e-12, (dt, flo, fhi, got, ref)
+    assert _lib.load().dvh_sos_pole_radius(None, 3) == -1.0

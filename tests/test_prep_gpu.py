@@ -51,12 +51,15 @@ def test_float32_record_keeps_its_dtype(device, case):
     assert np.abs(got.astype(np.float64) - ref).max() <= 2e-6 * np.abs(ref).max(), case
 
 
+@pytest.mark.parametrize("form", ["recursion", "matrix"])
 @pytest.mark.parametrize("n_rows,n_t,dtype,pad", [(640, 28000, np.float64, 0), (256, 140000, np.float32, 24)])
-def test_sosfiltfilt_long_blocks_and_strided_rows(device, n_rows, n_t, dtype, pad):
-    """dvh_sosfiltfilt with blocks longer than 32 samples (the block length grows with the record: L = 96 and 160
-    here, the bench record's 64 in between) and the longer A^L transition; the float32 case on rows of a wider
-    buffer (row stride n_t + 2 pad, the columns outside the rows untouched), through the C ABI.  Against
-    scipy.signal.sosfiltfilt as bandpass_data calls it (oracle/preprocess.py): 1e-10 in float64, 2e-6 in float32."""
+def test_sosfiltfilt_long_blocks_and_strided_rows(device, n_rows, n_t, dtype, pad, form):
+    """Both forms through the C ABI: dvh_sosfiltfilt (the block recursion, blocks longer than 32 samples: the block
+    length grows with the record, L = 96 and 160 here, with the longer A^L transition) and dvh_sosfiltfilt_planned
+    (the matrix-pipe form: 64-sample blocks, a record past the LDS-resident scan's 240 blocks, so its staged scan);
+    the float32 case on rows of a wider buffer (row stride n_t + 2 pad, the columns outside the rows untouched).
+    Against scipy.signal.sosfiltfilt as bandpass_data calls it (oracle/preprocess.py): 1e-10 in float64, 2e-6 in
+    float32."""
     import torch
 
     from das_diff_veh_amd import _lib
@@ -73,11 +76,34 @@ def test_sosfiltfilt_long_blocks_and_strided_rows(device, n_rows, n_t, dtype, pa
     sos, padlen, sos_t, zi_t = _design(dt, 1.2, 30, device)
     nbytes = int(_lib.load().dvh_sosfiltfilt_workspace(n_rows, n_t, len(sos), padlen))
     work = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
-    _lib.call("dvh_sosfiltfilt", _lib.ptr(rows), 0 if dtype == np.float32 else 1, n_rows, rows.stride(0), n_t,
-              _lib.ptr(sos_t), len(sos), padlen, _lib.ptr(zi_t), _lib.ptr(work), _lib.stream_of(device))
+    if form == "recursion":
+        _lib.call("dvh_sosfiltfilt", _lib.ptr(rows), 0 if dtype == np.float32 else 1, n_rows, rows.stride(0), n_t,
+                  _lib.ptr(sos_t), len(sos), padlen, _lib.ptr(zi_t), _lib.ptr(work), _lib.stream_of(device))
+    else:
+        plan = torch.empty(int(_lib.load().dvh_sosfiltfilt_plan_bytes(len(sos))) // 8, dtype=torch.float64,
+                           device=device)
+        _lib.call("dvh_sosfiltfilt_plan", _lib.ptr(sos_t), len(sos), _lib.ptr(zi_t), n_t, padlen, _lib.ptr(plan),
+                  _lib.stream_of(device))
+        _lib.call("dvh_sosfiltfilt_planned", _lib.ptr(rows), 0 if dtype == np.float32 else 1, n_rows, rows.stride(0),
+                  n_t, _lib.ptr(sos_t), len(sos), padlen, _lib.ptr(zi_t), _lib.ptr(plan), _lib.ptr(work),
+                  _lib.stream_of(device))
     got = dev.cpu().numpy()
     ref = oprep.bandpass_data_scipy(host.astype(np.float64), dt, 1.2, 30)
     tol = 1e-10 if dtype == np.float64 else 2e-6
     assert np.abs(got[:, pad:pad + n_t].astype(np.float64) - ref).max() <= tol * np.abs(ref).max()
     if pad:
         assert np.all(got[:, :pad] == 3.5) and np.all(got[:, pad + n_t:] == 3.5)
+
+
+def test_matrix_form_only_for_poles_clear_of_the_unit_circle(device):
+    """The drop-in plans the matrix-pipe form for the 1.2-30 Hz design (pole radius 0.9956) and takes the recursion
+    for 0.08-1 Hz (0.99973), whose block GEMMs would round to 5e-10 of the output (tests/test_disp_gpu.py's
+    bandpass cases hold both to 1e-10)."""
+    from das_diff_veh_amd import _lib
+    from das_diff_veh_amd import preprocess as pp
+    for (flo, fhi), planned in (((1.2, 30), True), ((0.08, 1), False)):
+        sos, padlen, sos_t, zi_t = pp._design(0.004, flo, fhi, device)
+        r = _lib.load().dvh_sos_pole_radius(np.ascontiguousarray(sos).ctypes.data, len(sos))
+        assert (r <= pp.SOS_MFMA_MAX_POLE) == planned, (flo, fhi, r)
+        plan = pp._plan((0.004, flo, fhi, str(device)), 3000, sos, padlen, sos_t, zi_t, device)
+        assert (plan is not None) == planned
