@@ -1321,9 +1321,12 @@ static int64_t table_bytes(int64_t n_pass) {
 static int launch_table(VsgArgs& A, int n, float2* tab, hipStream_t s) {
   const int grid = (int)std::min<int64_t>(((int64_t)A.n_pass + 3) / 4, 8 * (int64_t)cu_count());
   void* args[] = {&A, &tab};
+  // the engine's block tables + 4 waves' buffers (EngP1024's padded buffer A and stage tables included)
   if (n == 500)
-    return launch((const void*)vsg_pivot_table_kernel<EngF500>, grid, 4, sizeof(float2) * (500 + 4 * 1000), args, s);
-  return launch((const void*)vsg_pivot_table_kernel<EngP1024>, grid, 4, sizeof(float2) * (1024 + 4 * 2048), args, s);
+    return launch((const void*)vsg_pivot_table_kernel<EngF500>, grid, 4, EngF500::kBlockBytes + 4 * EngF500::kWaveBytes,
+                  args, s);
+  return launch((const void*)vsg_pivot_table_kernel<EngP1024>, grid, 4, EngP1024::kBlockBytes + 4 * EngP1024::kWaveBytes,
+                args, s);
 }
 
 DVH_API int64_t dvh_vsg_stack_workspace(int32_t n_pass, int32_t w) {

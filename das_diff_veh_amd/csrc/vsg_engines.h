@@ -856,6 +856,9 @@ struct EngF500 : FusedOps<EngF500, 8, 5> {
                         // 3 = also the XOR-swizzled layout (conflict-free stores, but its per-store address XORs cost
                         // more VALU than the conflicts: w = 499 synth10k launch 16.1 vs 15.65 ms)
 #endif
+#ifndef DVH_P1024_R16TW
+#define DVH_P1024_R16TW 1  // radix-16 stage twiddles from contiguous per-stage tables (0: strided reads of the main table)
+#endif
 struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   static constexpr int SW = DVH_P1024_SW;
   static constexpr int N = 1024;
@@ -868,7 +871,6 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   // LDS layout (lds_idx<SW>) of both buffers and the twiddle table with its contiguous stage tables (conflict-free
   // twiddle reads; with SW & 1 also conflict-free stage stores: the round-4 build spent 2.9 bank-conflict cycles per
   // LDS instruction on the Ls = 4 stores and the strided twiddle reads)
-  static constexpr size_t kBlockBytes = sizeof(float2) * tw_entries<N, SW>();  // twiddle tables
   // Radix-16 form (DVH_P1024_R16): forward = radix 16 (span 1, from the registers, zero-padded half) -> LDS A ->
   // radix 16 (span 16) -> LDS B -> the paired radix-4 last stage (span 256) in registers; inverse = radix 4 (span 1,
   // from the registers) -> LDS B -> radix 16 (span 4) -> LDS A -> radix 16 (span 64) -> Y in LDS B.  Two LDS round
@@ -879,9 +881,28 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   static constexpr bool R16 = DVH_P1024_R16 != 0;
   static constexpr int kBufA = R16 ? N + N / 16 : N;
   static constexpr size_t kWaveBytes = sizeof(float2) * (kBufA + N);         // buffers A and B
+  // Radix-16 stage twiddles, contiguous per stage after the tables above: stage Ls holds w^k, w^4k, w^8k (w = e^(-2 pi
+  // i Ls' / N), Ls' = N / (16 Ls)) for k < Ls at r16_tw(Ls) + {0, Ls, 2 Ls} + k, so that a stage's reads by lanes of
+  // consecutive k are consecutive (read from the main table at stride 4 k, 16 k, 32 k they cost 1.6 bank-conflict
+  // cycles per LDS instruction of the whole launch).
+  static constexpr int kR16Tw = tw_entries<N, SW>();
+  static constexpr int kR16TwEntries = R16 ? 3 * (16 + 4 + 64) : 0;
+  static constexpr int r16_tw(int Ls) { return kR16Tw + (Ls == 16 ? 0 : (Ls == 4 ? 48 : 60)); }
+  static constexpr size_t kBlockBytes = sizeof(float2) * (tw_entries<N, SW>() + kR16TwEntries);
 
   __device__ EngP1024(char* lds, int wave, int lane_) : FusedOps<EngP1024, 8, 9>(lds, wave, lane_, N / 2) {}
-  static __device__ void block_init(char* lds) { init_twiddles<N, SW>(reinterpret_cast<float2*>(lds)); }
+  static __device__ void block_init(char* lds) {
+    float2* t = reinterpret_cast<float2*>(lds);
+    init_twiddles<N, SW>(t);
+    for (int e = threadIdx.x; e < kR16TwEntries; e += blockDim.x) {
+      const int Ls = e < 48 ? 16 : (e < 60 ? 4 : 64), o = e - (Ls == 16 ? 0 : (Ls == 4 ? 48 : 60));
+      const int j = o / Ls, k = o % Ls, mult = j == 0 ? 1 : (j == 1 ? 4 : 8);
+      const int m = mult * k * (N / (16 * Ls));
+      double sn, cs;
+      sincospi(2.0 * (double)m / (double)N, &sn, &cs);  // init_twiddles' formula: the same float values as tw[m]
+      t[kR16Tw + e] = make_float2((float)cs, (float)(-sn));
+    }
+  }
 
   static __device__ __forceinline__ int bin(int l, int j) {
     switch (j) {
@@ -948,11 +969,16 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   template <int Ls, class IA, class OA>
   __device__ __forceinline__ void stage16(const float2* in, float2* out, IA ia, OA oa) const {
     const int i = lane, k = i % Ls;
-    constexpr int TWS = N / (16 * Ls);
     float2 a[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) a[t] = lds_ld(in, ia(i + 64 * t));
+#if DVH_P1024_R16TW
+    const float2* st = tw + r16_tw(Ls);
+    twiddle16(a, st[k], st[Ls + k], st[2 * Ls + k]);
+#else
+    constexpr int TWS = N / (16 * Ls);
     twiddle16(a, tw[k * TWS], tw[4 * k * TWS], tw[8 * k * TWS]);
+#endif
     dft16<false>(a);
     const int base = (i - k) * 16 + k;
 #pragma unroll
