@@ -383,20 +383,21 @@ template <int NS>
 struct SosmMats {
   static constexpr int NST = 2 * NS;
   static constexpr int h = 0, Hm = kSmL, g = Hm + kSmL * NST, M = g + kSmL * NST, Mzi = M + NST * NST,
-                       MQ = Mzi + NST, size = MQ + NST * NST;
+                       MQ = Mzi + NST, MQ16 = MQ + NST * NST, size = MQ16 + NST * NST;
 };
 constexpr int64_t sosm_plan_doubles(int n_sec) {
-  return kSmL + 2 * kSmL * (2 * n_sec) + 2 * (2 * n_sec) * (2 * n_sec) + 2 * n_sec;
+  return kSmL + 2 * kSmL * (2 * n_sec) + 3 * (2 * n_sec) * (2 * n_sec) + 2 * n_sec;
 }
 
 // Lanes e < NST: unit state e_e, zero input (Hm[:, e], M[:, e]); lane NST: zero state, unit sample (h, g).  Then
-// Mzi = M zi and MQ = M^Q by repeated products (threads (row, col) of the 20 x 20 result, LDS).
+// Mzi = M zi, MQ = M^Q and MQ16 = M^Q16 by repeated products (threads (row, col) of the 20 x 20 result, LDS): the
+// group transitions of the 8-group scans (sosm_scan_kernel, sosm_scanr_kernel) and the 16-group one (sosm_scanm).
 template <int NS>
 __global__ __launch_bounds__(512) void sosm_mats_kernel(const double* __restrict__ sos, const double* __restrict__ zi,
-                                                        int32_t Q, double* __restrict__ mats) {
+                                                        int32_t Q, int32_t Q16, double* __restrict__ mats) {
   using O = SosmMats<NS>;
   constexpr int NST = 2 * NS;
-  __shared__ double P[NST * NST], R[NST * NST];
+  __shared__ double P[NST * NST], R[NST * NST], M0[NST * NST];
   const int e = threadIdx.x;
   if (e <= NST) {
     SosCoef<NS> c;
@@ -433,34 +434,41 @@ __global__ __launch_bounds__(512) void sosm_mats_kernel(const double* __restrict
   const bool act = e < NST * NST;
   if (act) {
     mats[O::M + e] = P[e];
-    R[e] = row == col ? 1.0 : 0.0;  // R = M^0
+    M0[e] = P[e];
   }
   if (e < NST) {
     double a = 0.0;
     for (int j = 0; j < NST; ++j) a += P[e * NST + j] * zi[j];
     mats[O::Mzi + e] = a;
   }
-  // MQ = M^Q by binary powering: R *= P when the bit is set, P = P P
-  for (int q = Q; q > 0; q >>= 1) {
+  // M^q by binary powering: R *= P when the bit is set, P = P P (P restarts from M)
+  for (int pass = 0; pass < 2; ++pass) {
     __syncthreads();
-    if (q & 1) {
-      double a = 0.0;
-      if (act)
-        for (int j = 0; j < NST; ++j) a += R[row * NST + j] * P[j * NST + col];
-      __syncthreads();
-      if (act) R[e] = a;
-      __syncthreads();
+    if (act) {
+      P[e] = M0[e];
+      R[e] = row == col ? 1.0 : 0.0;  // R = M^0
     }
-    if (q > 1) {
-      double a = 0.0;
-      if (act)
-        for (int j = 0; j < NST; ++j) a += P[row * NST + j] * P[j * NST + col];
+    for (int q = pass == 0 ? Q : Q16; q > 0; q >>= 1) {
       __syncthreads();
-      if (act) P[e] = a;
+      if (q & 1) {
+        double a = 0.0;
+        if (act)
+          for (int j = 0; j < NST; ++j) a += R[row * NST + j] * P[j * NST + col];
+        __syncthreads();
+        if (act) R[e] = a;
+        __syncthreads();
+      }
+      if (q > 1) {
+        double a = 0.0;
+        if (act)
+          for (int j = 0; j < NST; ++j) a += P[row * NST + j] * P[j * NST + col];
+        __syncthreads();
+        if (act) P[e] = a;
+      }
     }
+    __syncthreads();
+    if (act) mats[(pass == 0 ? O::MQ : O::MQ16) + e] = R[e];
   }
-  __syncthreads();
-  if (act) mats[O::MQ + e] = R[e];
 }
 
 // sample i of row r of the forward pass's sequence: the odd extension of x (0 past n_ext)
@@ -1000,6 +1008,12 @@ __global__ __launch_bounds__(256) void sosm_bc_kernel(T* __restrict__ x, SosGeom
 // reads in flight: five round trips per step, 43 us per scan.)
 constexpr int kScanHW = 8, kScanPF = 16;
 __host__ __device__ constexpr int sosm_scan_q(int nb) { return nb > 2 ? (nb - 2 + kScanHW - 1) / kScanHW : 1; }
+// the 16-group scan on the matrix pipe (sosm_scanm_kernel): its group length, at most kScanMQ steps
+constexpr int kScanMG = 16, kScanMQ = 16;
+#ifndef DVH_SOS_SCANM
+#define DVH_SOS_SCANM 1  // the matrix-pipe scan where its 16 groups of <= 16 blocks cover the row (0: the VALU scans)
+#endif
+__host__ __device__ constexpr int sosm_scan_q16(int nb) { return nb > 2 ? (nb - 2 + kScanMG - 1) / kScanMG : 1; }
 
 template <int NS>
 __global__ __launch_bounds__(32 * kScanHW, 4) void sosm_scan_kernel(SosGeom G, const double* __restrict__ mats, int32_t Q,
@@ -1210,10 +1224,129 @@ __global__ __launch_bounds__(32 * kScanHW, 4) void sosm_scanr_kernel(SosGeom G, 
   }
 }
 
+// The same scan on the float64 matrix pipe, one wave per row: its 16 groups of Q16 <= 16 blocks are the 16 columns
+// of v_mfma_f64_16x16x4_f64 GEMMs, so a step of all 16 groups is M [NST x NST] times their states [NST x 16]: 2 row
+// tiles x KS k-steps.  Lane l holds fragment kk of column c = l & 15, state row 4 kk + (l >> 4), which is at once the
+// step's accumulator (tile kk / 4, register kk % 4) and the next step's B operand (k-step kk): the recurrence never
+// leaves the registers (the LDS broadcast of the VALU scans was their bound).  Level 1 keeps every group's Z in
+// registers (Q16 x KS doubles per lane), level 2 (the carries through M^Q16) runs on lanes 0 .. NST - 1 through the
+// LDS, level 3 adds M^(s + 1) C to the registers' Z and stores S as it goes.  E is read once (all loads of a lane
+// issued together at the start), S written once.  (Staging E and S through the LDS for whole-line transfers measured
+// slower, 31.5 against 28.1 us: the stores no longer overlap the steps.)
+template <int NS>
+__global__ __launch_bounds__(64, 1) void sosm_scanm_kernel(SosGeom G, const double* __restrict__ mats, int32_t Q,
+                                                          double* __restrict__ S) {
+  using O = SosmMats<NS>;
+  constexpr int NST = 2 * NS, KS = (NST + 3) / 4, TT = (NST + 15) / 16;
+  __shared__ __attribute__((aligned(16))) double zl[kScanMG][NST + (NST & 1)];
+  __shared__ __attribute__((aligned(16))) double carry[kScanMG][NST + (NST & 1)];
+  __shared__ __attribute__((aligned(16))) double slot[NST + (NST & 1)];
+  const int l = threadIdx.x, c = l & 15, q4 = l >> 4;
+  double* Sr = S + (int64_t)blockIdx.x * G.nb * NST;
+  const int K = G.nb - 1;
+  const int k0 = 1 + c * Q, k1 = min(1 + (c + 1) * Q, K);  // group c = [k0, k1)
+  const int len = max(k1 - k0, 0);
+  const int ng = K > 1 ? (K - 1 + Q - 1) / Q : 0;
+  // A operands: M[16 t + c][4 kk + q4] (zero outside NST x NST)
+  double a[TT][KS];
+#pragma unroll
+  for (int t = 0; t < TT; ++t)
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int r = 16 * t + c, k = 4 * kk + q4;
+      const double v = mats[O::M + min(r, NST - 1) * NST + min(k, NST - 1)];
+      a[t][kk] = (r < NST && k < NST) ? v : 0.0;
+    }
+  // E of every step of the group, fragment kk = row 4 kk + q4 (rows past NST and steps past the group: any finite
+  // value of the row, never used)
+  double z[kScanMQ][KS];
+#pragma unroll
+  for (int st = 0; st < kScanMQ; ++st)
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int k = min(k0 + st, K - 1), r = min(4 * kk + q4, NST - 1);
+      z[st][kk] = Sr[(int64_t)k * NST + r];
+    }
+  double b[KS];  // the state entering the step (B operand): S[0] for group 0, zero for the others
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const double v = Sr[min(4 * kk + q4, NST - 1)];
+    b[kk] = (c == 0 && 4 * kk + q4 < NST) ? v : 0.0;
+  }
+  auto step = [&](double (&v)[KS], const double* cin) {  // v = cin + M b (cin: KS fragments, or zero), b = v
+    doublex4_t acc[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) acc[t][rr] = (cin && 4 * t + rr < KS) ? cin[4 * t + rr] : 0.0;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+      for (int t = 0; t < TT; ++t) acc[t] = mfma_f64x4(a[t][kk], b[kk], acc[t]);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      v[kk] = acc[kk >> 2][kk & 3];
+      b[kk] = v[kk];
+    }
+  };
+  // level 1: Z in place of E
+#pragma unroll
+  for (int st = 0; st < kScanMQ; ++st)
+    if (st < Q) step(z[st], z[st]);
+  // the groups' last Z -> LDS
+#pragma unroll
+  for (int st = 0; st < kScanMQ; ++st)
+    if (st == len - 1)
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+        if (4 * kk + q4 < NST) zl[c][4 * kk + q4] = z[st][kk];
+  __syncthreads();
+  // level 2: C_0 = Z_last(0), C_g = Z_last(g) + M^Q16 C_(g - 1), lanes j < NST
+  if (l < NST) {
+    double mq[NST];
+#pragma unroll
+    for (int i = 0; i < NST; ++i) mq[i] = mats[O::MQ16 + l * NST + i];
+    double cv = zl[0][l];
+    carry[0][l] = cv;
+    for (int g = 1; g + 1 < ng; ++g) {
+      slot[l] = cv;
+      wave_barrier_lds();
+      double acc = zl[g][l];
+#pragma unroll
+      for (int i = 0; i < NST; ++i) acc += mq[i] * slot[i];
+      wave_barrier_lds();
+      cv = acc;
+      carry[g][l] = cv;
+    }
+  }
+  __syncthreads();
+  // level 3: D = M^(s + 1) C_(c - 1) (zero for group 0), S = Z + D
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const int r = 4 * kk + q4;
+    const double v = carry[c > 0 ? c - 1 : 0][min(r, NST - 1)];
+    b[kk] = (c > 0 && c < ng && r < NST) ? v : 0.0;
+  }
+#pragma unroll
+  for (int st = 0; st < kScanMQ; ++st) {
+    if (st < Q) {
+      double d[KS];
+      step(d, nullptr);
+      if (st < len)
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+          if (4 * kk + q4 < NST) Sr[(int64_t)(k0 + st) * NST + 4 * kk + q4] = z[st][kk] + d[kk];
+    }
+  }
+}
+
 template <int NS>
 static void sosm_scan(const SosGeom& G, const double* plan, int Q, double* S, hipStream_t st) {
   if (G.nb <= 2) return;
-  if ((int64_t)(G.nb - 1) * 2 * NS <= kScanCap)
+  if (DVH_SOS_SCANM && sosm_scan_q16(G.nb) <= kScanMQ)
+    hipLaunchKernelGGL(sosm_scanm_kernel<NS>, dim3((unsigned)G.n_rows), dim3(64), 0, st, G, plan,
+                       (int32_t)sosm_scan_q16(G.nb), S);
+  else if ((int64_t)(G.nb - 1) * 2 * NS <= kScanCap)
     hipLaunchKernelGGL(sosm_scanr_kernel<NS>, dim3((unsigned)G.n_rows), dim3(32 * kScanHW), 0, st, G, plan, Q, S);
   else
     hipLaunchKernelGGL(sosm_scan_kernel<NS>, dim3((unsigned)G.n_rows), dim3(32 * kScanHW), 0, st, G, plan, Q, S);
@@ -1234,14 +1367,15 @@ static SosGeom sosm_geom(int64_t n_rows, int64_t row_stride, int32_t n_t, int32_
 // workspace of the MFMA path: y [n_rows][n_ext] + Sf, Sb [n_rows][nb][2 n_sec] + the plan (operator table), doubles
 static int64_t sosm_workspace_doubles(const SosGeom& G, int n_sec) {
   const int64_t nst = 2 * n_sec;
-  return G.n_rows * G.n_ext + 2 * G.n_rows * G.nb * nst + sosm_plan_doubles(n_sec);
+  return ((G.n_rows * G.n_ext + 1) & ~1LL) + 2 * G.n_rows * G.nb * nst + sosm_plan_doubles(n_sec);  // Sf 16-byte aligned
 }
 // the MFMA path's column indices are 32-bit
 static bool sosm_fits(const SosGeom& G) { return G.n_rows * (int64_t)G.nb < (1LL << 31) - 16; }
 
 template <int NS>
 static void sosm_plan(const double* sos, const double* zi, const SosGeom& G, double* plan, hipStream_t st) {
-  hipLaunchKernelGGL(sosm_mats_kernel<NS>, dim3(1), dim3(512), 0, st, sos, zi, (int32_t)sosm_scan_q(G.nb), plan);
+  hipLaunchKernelGGL(sosm_mats_kernel<NS>, dim3(1), dim3(512), 0, st, sos, zi, (int32_t)sosm_scan_q(G.nb),
+                     (int32_t)sosm_scan_q16(G.nb), plan);
 }
 
 template <typename T, int NS>
@@ -1249,7 +1383,7 @@ static int sosm_run(T* x, const SosGeom& G, const double* sos, const double* zi,
                     hipStream_t st) {
   constexpr int NST = 2 * NS;
   double* y = work;
-  double* Sf = y + G.n_rows * G.n_ext;
+  double* Sf = y + ((G.n_rows * G.n_ext + 1) & ~1LL);  // 16-byte aligned (the scans' 16-byte loads)
   double* Sb = Sf + G.n_rows * G.nb * NST;
   const int Q = sosm_scan_q(G.nb);
   // persistent grids: the blocks that are resident at once (LDS and registers), each wave looping over tiles, so
@@ -1292,7 +1426,7 @@ template <typename T, int NS>
 static int sosfiltfilt_mfma(T* x, const SosGeom& G, const double* sos, const double* zi, const double* plan, double* work,
                             hipStream_t st) {
   if (!plan) {
-    double* p = work + G.n_rows * G.n_ext + 2 * G.n_rows * G.nb * (2 * NS);
+    double* p = work + ((G.n_rows * G.n_ext + 1) & ~1LL) + 2 * G.n_rows * G.nb * (2 * NS);
     sosm_plan<NS>(sos, zi, G, p, st);
     plan = p;
   }

@@ -201,8 +201,8 @@ int dvh_ridge(const float* fv, int64_t b_stride, int32_t B, int32_t nV, int32_t 
 /* scipy.signal.sosfiltfilt(sos, x, axis=-1) per row (bandpass_data, modules/utils.py:179-189);
  * zi = sosfilt_zi(sos) [n_sec][2] (device); n_sec <= 16.  Time-parallel: each row is filtered in blocks
  * (zero-state block filters, a scan of the 2 n_sec block states, re-filter), forward then backward, the blocks by
- * the filter's own recursion (any stable design).  work: device buffer of dvh_sosfiltfilt_workspace(n_rows, n_t,
- * n_sec, padlen) bytes. */
+ * the filter's own recursion (any stable design).  work: 16-byte aligned device buffer of
+ * dvh_sosfiltfilt_workspace(n_rows, n_t, n_sec, padlen) bytes. */
 int64_t dvh_sosfiltfilt_workspace(int64_t n_rows, int32_t n_t, int32_t n_sec, int32_t padlen);
 int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, int32_t n_t, const double* sos,
                     int32_t n_sec, int32_t padlen, const double* zi, double* work, void* stream);
