@@ -644,7 +644,12 @@ __device__ __forceinline__ void sosm_acc_to_lds(double* img, int lane, const dou
     for (int rr = 0; rr < 4; ++rr) img[(lane & 15) * kSmLd + 16 * t + 4 * rr + (lane >> 4)] = acc[t][rr];
 }
 
-// state accumulators (rows m = 16 t + 4 rr + (l >> 4)) -> the LDS image as [column][NST]
+// state accumulators (rows m = 16 t + 4 rr + (l >> 4)) -> the LDS image as [column][sosm_stp(NST)]: an odd row
+// stride, so that the 16 columns of a write land in 16 distinct bank pairs (at NST = 20 they fell on 4: 4-way
+// conflicts); element (column, m) is read back at sosm_sv(v) for v = column NST + m
+__host__ __device__ constexpr int sosm_stp(int nst) { return nst | 1; }
+template <int NST>
+__device__ __forceinline__ int sosm_sv(int v) { return (v / NST) * sosm_stp(NST) + v % NST; }
 template <int NST>
 __device__ __forceinline__ void sosm_states_out(double* img, int lane, const doublex4_t (&e)[2]) {
 #pragma unroll
@@ -652,7 +657,7 @@ __device__ __forceinline__ void sosm_states_out(double* img, int lane, const dou
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int m = 16 * t + 4 * rr + (lane >> 4);
-      if (m < NST) img[(lane & 15) * NST + m] = e[t][rr];
+      if (m < NST) img[(lane & 15) * sosm_stp(NST) + m] = e[t][rr];
     }
 }
 
@@ -721,7 +726,7 @@ __global__ __launch_bounds__(256) void sosm_fa_kernel(const T* __restrict__ x, S
 #pragma unroll
       for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
         const int v = lane + 64 * u;
-        if (v < 16 * NST) sp[v] = img[v];
+        if (v < 16 * NST) sp[v] = img[sosm_sv<NST>(v)];
       }
     } else {
 #pragma unroll
@@ -730,7 +735,7 @@ __global__ __launch_bounds__(256) void sosm_fa_kernel(const T* __restrict__ x, S
         if (v < 16 * NST) {
           int rc, kc;
           sosm_col(tl, v / NST, G.nb, rc, kc);
-          if (rc < nr && kc < G.nb - 1) Sf[((int64_t)rc * G.nb + kc) * NST + v % NST] = img[v];
+          if (rc < nr && kc < G.nb - 1) Sf[((int64_t)rc * G.nb + kc) * NST + v % NST] = img[sosm_sv<NST>(v)];
         }
       }
     }
@@ -851,7 +856,7 @@ __global__ __launch_bounds__(256) void sosm_fc_kernel(const T* __restrict__ x, S
 #pragma unroll
       for (int u = 0; u < (16 * NST + 63) / 64; ++u) {
         const int v = lane + 64 * u;
-        if (v < 16 * NST) sp[v % NST - (v / NST) * NST] = img[v];
+        if (v < 16 * NST) sp[v % NST - (v / NST) * NST] = img[sosm_sv<NST>(v)];
       }
     } else {
 #pragma unroll
@@ -860,7 +865,7 @@ __global__ __launch_bounds__(256) void sosm_fc_kernel(const T* __restrict__ x, S
         if (v < 16 * NST) {
           int rc, kc;
           sosm_col(tl, v / NST, G.nb, rc, kc);
-          if (rc < nr && kc < G.nb - 1) Sb[((int64_t)rc * G.nb + (G.nb - 1 - kc)) * NST + v % NST] = img[v];
+          if (rc < nr && kc < G.nb - 1) Sb[((int64_t)rc * G.nb + (G.nb - 1 - kc)) * NST + v % NST] = img[sosm_sv<NST>(v)];
         }
       }
     }
