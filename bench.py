@@ -982,15 +982,15 @@ def prep_main(args, world, rank, device):
         "trace_samples_per_s": world * args.steps * n_ch * n_t / elapsed,
         "roofline": {"bound": "fp64-valu", "achieved": flop / bp / 1e12, "peak": FP64_VALU_SPEC_TF, "unit": "TFLOP/s",
                      "frac": flop / bp / 1e12 / FP64_VALU_SPEC_TF, "traffic": None,
-                     "kernel": "dvh_sosfiltfilt (sosm_fa / sosm_scan / sosm_fc / sosm_bf / sosm_scan / sosm_bc: "
-                               "block GEMMs on the float64 MFMA pipe, two-level state scans)",
+                     "kernel": "dvh_sosfiltfilt_planned (sosm_fa / sosm_scanm / sosm_fc / sosm_bf / sosm_scanm / "
+                               "sosm_bc: block GEMMs and two-level state scans on the float64 MFMA pipe)",
                      "launch_ms": bp * 1e3, "flop_model": "9 flops per sample per section (scipy sosfilt), forward + "
                                                           "backward over n_t + 2 padlen (the sequential filter's work)",
                      "mfma_flop_issued": mfma_flop, "mfma_achieved_tflops": mfma_flop / bp / 1e12,
                      "mfma_frac_of_spec": mfma_flop / bp / 1e12 / FP64_MFMA_SPEC_TF,
                      "mfma_model": "64-sample blocks as float64 MFMA GEMMs: 184 v_mfma_f64_16x16x4_f64 per 16 blocks "
                                    "(forward end states 32, forward outputs + backward end states 92, backward outputs "
-                                   "60), the state scans between them on the VALU",
+                                   "60); the state scans' own MFMAs (10 per step of 16 groups) not counted",
                      "hbm_bytes_model": "record read + y (f64) written and read + record written",
                      "hbm_frac": (2 * rec_bytes + 16.0 * n_ch * n_ext) / bp / 1e9 / HBM_PEAK_GBS},
         "kernels_ms": {"bandpass": bp * 1e3, "trace_cleanup": cl * 1e3},
