@@ -408,7 +408,7 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
                                              float* __restrict__ stack, int64_t t0, int64_t stride,
-                                             uint32_t* tq = nullptr) {
+                                             uint32_t* tq = nullptr, uint32_t* started = nullptr) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -423,6 +423,7 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
   int64_t tn = tq ? pull_unit(tq, lane_t) : t0;
   for (int64_t t = tn; t < n_task; t = tn) {
     tn = tq ? (int64_t)pull_unit(tq, lane_t) : t + stride;
+    if (started && lane_t == 0) atomicAdd(started, 1u);  // the scan's pacing (DVH_SCAN_PACE)
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
     int np = -1, ni = 0;
@@ -558,7 +559,7 @@ __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const flo
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
                                              float* __restrict__ stack, int64_t t0, int64_t stride,
-                                             uint32_t* tq = nullptr) {
+                                             uint32_t* tq = nullptr, uint32_t* started = nullptr) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -860,10 +861,20 @@ struct ScanArgs {
 };
 
 // Pull scan units (window, kScanRows channel rows) until none is left; atomicMax into vflag[window].
+// Pacing (DVH_SCAN_PACE = L > 0, fused launches of the exact engines): the unit of window q waits until the correlation
+// has started the tasks of chunk q n_chunk / n_pass - L, so that the scan streams the windows the correlation is
+// loading instead of running ahead of it.
+#ifndef DVH_SCAN_PACE
+#define DVH_SCAN_PACE 0
+#endif
+struct ScanPace {
+  const uint32_t* started = nullptr;  // correlation tasks started
+  int64_t n_chunk = 0, n_pass = 1, R = 0;
+};
 template <int D = kScanDepth>
 __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, uint32_t* __restrict__ vflag,
                                            uint32_t* __restrict__ counter, int lane,
-                                           const int32_t* __restrict__ sorder = nullptr) {
+                                           const int32_t* __restrict__ sorder = nullptr, ScanPace pace = ScanPace{}) {
   const int upp = (S.n_ch + kScanRows - 1) / kScanRows;  // units per window
   const int n_units = S.n_win * upp;
   const bool vec = (S.n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
@@ -872,6 +883,11 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
   while (u < n_units) {
     const int un = pull_unit(counter, lane);  // the next unit's index, fetched under this unit's loads
     const int q = u / upp, c0 = (u - q * upp) * kScanRows;
+    if (pace.started) {
+      const int64_t need = min((q * pace.n_chunk / pace.n_pass - DVH_SCAN_PACE) * pace.R, pace.n_chunk * pace.R);
+      while ((int64_t)__hip_atomic_load(pace.started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
+        __builtin_amdgcn_s_sleep(4);
+    }
     const int s = (sorder && !S.tab) ? sld(sorder + q) : q;
     const float* base = S.tab ? A.win + (int64_t)sld(S.tab + s) * A.ch_stride : A.win + (int64_t)s * A.pass_stride;
     const uint32_t m = scan_rows<D>(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
@@ -1016,8 +1032,8 @@ template <class E, bool EXACT>
 __device__ __forceinline__ void stack_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                             const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                             int32_t n_chunk, const float* __restrict__ weight, float* __restrict__ stack,
-                                            int64_t t0, int64_t stride, uint32_t* tq) {
-  if constexpr (EXACT) stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq);
+                                            int64_t t0, int64_t stride, uint32_t* tq, uint32_t* started = nullptr) {
+  if constexpr (EXACT) stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq, started);
   else stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq);
 }
 
@@ -1044,15 +1060,23 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
 #endif
     stack_tasks<E, EXACT>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
-                          (int64_t)gridDim.x * kFft, kPull ? counter + 1 : nullptr);
+                          (int64_t)gridDim.x * kFft, kPull ? counter + 1 : nullptr,
+                          (DVH_SCAN_PACE > 0 && EXACT && !kPull) ? counter + 1 : nullptr);
 #if DVH_CORR_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
   }
   // the chunks cover order[0, end of the last chunk): scan in that order when it lists every pass
   const int32_t* sorder = (n_chunk > 0 && sld(chunk_tab + 3 * (n_chunk - 1) + 1) == A.n_pass) ? order : nullptr;
+  ScanPace pace;
+  if (DVH_SCAN_PACE > 0 && EXACT && !kPull && sorder && !S.tab && wave >= kFft) {  // scan waves only
+    pace.started = counter + 1;
+    pace.n_chunk = n_chunk;
+    pace.n_pass = A.n_pass;
+    pace.R = A.R;
+  }
   if (skip) scan_units_skip(A, S, vflag, counter, lane, sorder);
-  else scan_units<kDepth>(A, S, vflag, counter, lane, sorder);
+  else scan_units<kDepth>(A, S, vflag, counter, lane, sorder, pace);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
