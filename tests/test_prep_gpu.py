@@ -107,3 +107,22 @@ def test_matrix_form_only_for_poles_clear_of_the_unit_circle(device):
         assert (r <= pp.SOS_MFMA_MAX_POLE) == planned, (flo, fhi, r)
         plan = pp._plan((0.004, flo, fhi, str(device)), 3000, sos, padlen, sos_t, zi_t, device)
         assert (plan is not None) == planned
+
+
+@pytest.mark.parametrize("n_t", [130, 700, 4000, 15500, 16600])
+def test_matrix_form_record_lengths(device, n_t):
+    """The matrix-pipe form across the scans it dispatches to: records of 4 blocks (one group holds every block),
+    mid-size records (groups of 1-3 blocks, some of the 16 groups empty), 15 500 samples (16 groups of 16 blocks, the
+    last partial: the matrix-pipe scan's limit) and 16 600 (past it: the staged scan), float64 rows against
+    scipy.signal.sosfiltfilt as bandpass_data calls it (1e-10)."""
+    import torch
+
+    from das_diff_veh_amd.preprocess import bandpass_inplace
+    from oracle import preprocess as oprep
+    rng = np.random.default_rng(n_t)
+    dt = 0.004
+    host = rng.standard_normal((48, n_t)) + np.sin(2 * np.pi * 7.0 * np.arange(n_t) * dt)[None, :]
+    dev = torch.from_numpy(host.copy()).to(device)
+    bandpass_inplace(dev, dt, 1.2, 30)
+    ref = oprep.bandpass_data_scipy(host, dt, 1.2, 30)
+    assert np.abs(dev.cpu().numpy() - ref).max() <= 1e-10 * np.abs(ref).max()
