@@ -1801,6 +1801,7 @@ DVH_API int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_
                             const double* sos, int32_t n_sec, int32_t padlen, const double* zi, double* work,
                             void* stream) {
   if (!x || !sos || !zi || !work) return set_error(-2, "null pointer argument");
+  if (reinterpret_cast<uintptr_t>(work) % 16) return set_error(-2, "work must be 16-byte aligned");
   if (n_sec <= 0 || n_sec > kMaxSec) return set_error(-4, "unsupported number of second-order sections");
   if (n_t <= padlen) return set_error(-4, "The length of the input vector x must be greater than padlen");
   if (padlen < 0 || n_t < 2) return set_error(-2, "invalid padlen / length");
@@ -1815,6 +1816,7 @@ DVH_API int dvh_sosfiltfilt_planned(void* x, int32_t dtype, int64_t n_rows, int6
                                     const double* sos, int32_t n_sec, int32_t padlen, const double* zi, const double* plan,
                                     double* work, void* stream) {
   if (!x || !sos || !zi || !work) return set_error(-2, "null pointer argument");  // plan NULL: the recursion
+  if (reinterpret_cast<uintptr_t>(work) % 16) return set_error(-2, "work must be 16-byte aligned");
   if (n_sec <= 0 || n_sec > kMaxSec) return set_error(-4, "unsupported number of second-order sections");
   if (n_t <= padlen) return set_error(-4, "The length of the input vector x must be greater than padlen");
   if (padlen < 0 || n_t < 2) return set_error(-2, "invalid padlen / length");

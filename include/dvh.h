@@ -209,8 +209,8 @@ int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, 
 /* The matrix-pipe form: the blocks as float64 MFMA GEMMs with the block operators (impulse response, zero-input
  * responses, state responses, the block and group transitions), formed once per filter design and record length n_t
  * (they depend on n_t + 2 padlen through the scan's group size): plan = device buffer of dvh_sosfiltfilt_plan_bytes(
- * n_sec) bytes.  dvh_sosfiltfilt_planned filters with them (work: dvh_sosfiltfilt_workspace bytes; plan NULL: the
- * recursion, as dvh_sosfiltfilt).  Its rounding grows with the largest pole radius r (host sos: dvh_sos_pole_radius):
+ * n_sec) bytes.  dvh_sosfiltfilt_planned filters with them (work: 16-byte aligned, dvh_sosfiltfilt_workspace bytes;
+ * plan NULL: the recursion, as dvh_sosfiltfilt).  Its rounding grows with the largest pole radius r (host sos: dvh_sos_pole_radius):
  * 1e-13 relative at r = 0.9956, 5e-10 at r = 0.99973, so plan it only for r <= DVH_SOS_MFMA_MAX_POLE.
  * bandpass_data (modules/utils.py:179-189) called once per record of the same shape designs the same filter every
  * time; the drop-in caches the plan per (design, n_t). */

@@ -590,3 +590,15 @@ def test_sos_pole_radius_matches_numpy_roots():
         got = _lib.load().dvh_sos_pole_radius(sos.ctypes.data, len(sos))
         assert abs(got - ref) < 1e-12, (dt, flo, fhi, got, ref)
     assert _lib.load().dvh_sos_pole_radius(None, 3) == -1.0
+
+
+def test_sosfiltfilt_rejects_misaligned_workspace():
+    """The state scans move 16-byte pieces of the workspace: a misaligned one is an argument error, reported before
+    any device work (no GPU needed to check it)."""
+    from das_diff_veh_amd import _lib
+    lib = _lib.load()
+    fake = ctypes.c_void_p(0x1000)
+    for name, extra in (("dvh_sosfiltfilt", ()), ("dvh_sosfiltfilt_planned", (None,))):
+        args = (fake, 0, 4, 3000, 3000, fake, 10, 63, fake) + extra + (ctypes.c_void_p(0x1008), None)
+        assert getattr(lib, name)(*args) == -2
+        assert b"16-byte aligned" in lib.dvh_last_error()
