@@ -64,10 +64,12 @@ class ImagesFromWindows:
 
     def save_images(self, fig_folder, file_prefix):
         """apis/imaging_classes.py:110-117: one figure per image and one of the mean, by the images' plot_image
-        (plotting is outside the accelerated path: the image classes' plot_image raises with a pointer)."""
-        for k, image in enumerate(self.images):
-            image.plot_image(f"{file_prefix}{k}.png", norm=True, fig_folder=fig_folder)
-        self.avg_image.plot_image(f"{file_prefix}_avg.png", norm=True, fig_folder=fig_folder)
+        (plotting is outside the accelerated path: raises with a pointer before any per-pass image is formed)."""
+        raise NotImplementedError(
+            "plotting is outside the accelerated path (apis/imaging_classes.py:110-117 plots every image); use the "
+            "reference's plot_xcorr / plot_fv_map on images[k] and avg_image"
+            + ("" if getattr(self, "images", None) is not None else
+               " (the per-pass images were not formed: get_images(shard_over_ranks=True) keeps only avg_image)"))
 
 
 class DispersionImagesFromWindows(ImagesFromWindows):

@@ -310,15 +310,6 @@ __global__ __launch_bounds__(256) void fv_kernel(const double* __restrict__ FK, 
 // both sides, and the Savitzky-Golay pass gives every thread 4 consecutive outputs of one velocity
 // (28 inputs read as 7 x 16 B, 25 taps each in double, the same tap order as fv_kernel).  Bound:
 // float64 FMA issue (25 per output) and the 4 B/output HBM write.
-#ifndef DVH_FV_LEGACY
-#define DVH_FV_LEGACY 0  // 1: always the per-image fv_kernel (A/B builds)
-#endif
-#ifndef DVH_FV_TILE
-#define DVH_FV_TILE 1    // default: the frequency-tiled kernel (DVH_FV_TILE=0 at run time selects the others)
-#endif
-#ifndef DVH_FV_BATCH
-#define DVH_FV_BATCH 1   // default dispatch of the batched kernel (DVH_FV_G=<images per block> selects it at run time)
-#endif
 constexpr int kFvThreads = 1024;
 constexpr int kFvVT = 4;   // velocities per thread in the sampling phase
 constexpr int kFvPre = 4;  // FK doubles prefetched per thread: grids up to 4 x 1024 bins
@@ -508,9 +499,7 @@ __global__ __launch_bounds__(kFvThreads) void fv_batch_kernel(
 // the 25 samples the right-edge fit reads), so the Savitzky-Golay pass of its outputs is local.
 // Only the FK columns the tile's frequencies touch are staged per image.
 constexpr int kTileThreads = 256;
-#ifndef DVH_FV_TILE_VT
-#define DVH_FV_TILE_VT 4  // velocities per fv_tile block (4 or 8): more outputs per barrier pair, more registers
-#endif
+constexpr int kTileVT = 4;  // velocities per fv_tile block (8: more outputs per barrier pair, more registers)
 
 // kCells: instead of every FK row of the columns the tile touches, the block stages only the cells its
 // bilinear stencils read (host tables of DispPlan.cell_tables, per (velocity chunk, tile) ct: the cells'
@@ -760,19 +749,8 @@ __global__ __launch_bounds__(kTileThreads) void fv_tile_kernel(
 // bit-identical to what the other kernels compute.  (Forming the weights in the kernel from the query and
 // LDS tables of the k grid and fw measured slower: 1 207 vs 704 us for one image per wave, the LDS
 // bandwidth of the extra reads.)  Two images per wave (GI = 2) measured 673 vs 724 us for one.
-#ifndef DVH_FV_MF_GI
-#define DVH_FV_MF_GI 2  // images per wave in lock step (1 or 2)
-#endif
-#ifndef DVH_FV_MF_LATE
-#define DVH_FV_MF_LATE 0  // 1: a tile's table loads issued after the previous ones are consumed (half the
-                          // in-flight registers, a shorter load-to-use distance)
-#endif
-#ifndef DVH_FV_NT_STORE
-#define DVH_FV_NT_STORE 0  // 1: the f-v tiles stored non-temporally (A/B of the write traffic)
-#endif
-#ifndef DVH_FV_MF_WPE
-#define DVH_FV_MF_WPE (DVH_FV_MF_GI == 1 ? 3 : 2)  // waves per SIMD the kernel is register-budgeted for
-#endif
+constexpr int kMfGI = 2;   // images per wave in lock step
+constexpr int kMfWpe = 2;  // waves per SIMD the kernel is register-budgeted for
 constexpr int kMfV = 16;      // velocities per wave
 constexpr int kMfWaves = 4;   // waves per block
 
@@ -801,7 +779,7 @@ __host__ __device__ inline size_t fv_mfma_lds(int GI, int nfk) {
 }
 
 template <int GI>
-__global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(DVH_FV_MF_WPE, DVH_FV_MF_WPE))) void fv_mfma_kernel(
+__global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(kMfWpe, kMfWpe))) void fv_mfma_kernel(
     const double* __restrict__ FK, int32_t B, int32_t G, int32_t n_kb, int32_t n_fb, const double2* __restrict__ hx,
     const int32_t* __restrict__ cb, int32_t nF, int32_t nV, const double2* __restrict__ fw, const double* __restrict__ sg,
     float* __restrict__ fv, int32_t n_vb, int32_t xcd_map) {
@@ -923,13 +901,7 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int v = vw + kk_ + 4 * r;
-          if (v < nV_) {
-#if DVH_FV_NT_STORE
-            __builtin_nontemporal_store((float)acc[g][r], out_b + (int64_t)v * nF_ + f);
-#else
-            out_b[(int64_t)v * nF_ + f] = (float)acc[g][r];
-#endif
-          }
+          if (v < nV_) out_b[(int64_t)v * nF_ + f] = (float)acc[g][r];
         }
       }
     };
@@ -973,16 +945,6 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
       for (int u = 0; u < 4; ++u) {
         const int t = t0 + u;
         if (t >= t_reg) break;
-#if DVH_FV_MF_LATE
-        // steps 4 t + 10 + i -> slot (4 (u + 1) + 10 + i) & 15  (t = t0 + u, t0 = 1 mod 4), then the next
-        // tile's table loads into the same registers (in flight during this tile's MFMAs)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          tfinish(pd[i], x[(4 * (u + 1) + 10 + i) & 15]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pd[i] = tload(16 * t + 44 + 4 * i + kk_);
-#else
         Pend nx[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) nx[i] = tload(16 * t + 44 + 4 * i + kk_);
@@ -991,7 +953,6 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
         for (int i = 0; i < 4; ++i) {
           tfinish(pd[i], x[(4 * (u + 1) + 10 + i) & 15]);
         }
-#endif
         doublex4 acc[GI];
 #pragma unroll
         for (int g = 0; g < GI; ++g) acc[g] = doublex4{0.0, 0.0, 0.0, 0.0};
@@ -1004,10 +965,8 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(D
           }
         }
         store(acc, kMfV * t, fl_);
-#if !DVH_FV_MF_LATE
 #pragma unroll
         for (int i = 0; i < 4; ++i) pd[i] = nx[i];
-#endif
         // one tile per scheduling region, its samples finished in it
         asm volatile("" ::"v"(x[(4 * (u + 1) + 10) & 15][0]), "v"(x[(4 * (u + 1) + 11) & 15][0]),
                      "v"(x[(4 * (u + 1) + 12) & 15][0]), "v"(x[(4 * (u + 1) + 13) & 15][0]));
@@ -1133,11 +1092,11 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
     int TO = (nF + nt - 1) / nt;
     TO = (TO + 3) & ~3;
     const int last = nF - (nt - 1) * TO;
-    int mode = DVH_FV_TILE;
+    int mode = 1;  // the frequency-tiled kernel where it pays (below)
     if (const char* ev = getenv("DVH_FV_TILE")) mode = atoi(ev);  // A/B: 0 = batched / per-image, 2 = always tiled
     const size_t lds_t = sizeof(double) * (size_t)(((size_t)n_kb * n_fb + 1) & ~(size_t)1) +
                          sizeof(double) * (size_t)((sgl * sgl + 1) & ~1) +
-                         sizeof(float) * (size_t)DVH_FV_TILE_VT * (2 * kSgPad + kTileThreads + 4);
+                         sizeof(float) * (size_t)kTileVT * (2 * kSgPad + kTileThreads + 4);
     // large batches of long frequency axes only: on few images (the bench's 3 class stacks of
     // 1 000 x 242) the per-image kernel measured faster (1.100 vs 1.125 ms per bench step), and with
     // tiles under 160 outputs (nF = 242: 2 x 124) half the block idles -- the batched kernel packs
@@ -1145,7 +1104,7 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
     const int64_t work = (int64_t)B * nt * ((nV + kFvVT - 1) / kFvVT);  // in 4-velocity units
     if (mode && ((work >= 8192 && TO >= 160) || mode > 1) && last >= kSgPad + 1 && TO + 2 * kSgPad <= kTileThreads &&
         nF >= sgl && lds_t <= 64 * 1024) {
-      constexpr int VT = DVH_FV_TILE_VT;
+      constexpr int VT = kTileVT;
       hipError_t e = hipFuncSetAttribute((const void*)fv_tile_kernel<VT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)lds_t);
       if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
@@ -1163,7 +1122,7 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
   }
   int n_grp = nF <= kFvThreads ? kFvThreads / nF : 0;
   n_grp = n_grp > 8 ? 8 : n_grp;
-  if (!DVH_FV_LEGACY && n_grp > 0) {
+  if (n_grp > 0) {
     const int VC = kFvVT * n_grp;
     const size_t lds_b = 2 * sizeof(double) * (size_t)(((size_t)n_kb * n_fb + 1) & ~(size_t)1) +
                          sizeof(double) * (size_t)((sgl * sgl + 1) & ~1) + sizeof(float) * (size_t)VC * (((nF + 3) & ~3) + 2 * kSgPad);
@@ -1178,7 +1137,7 @@ DVH_API int dvh_disp_fv(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb,
       // per-image kernel's 256-thread blocks fill the chip better
       int G = (int)(((int64_t)B * nvc + 1023) / 1024);
       G = G < 1 ? 1 : (G > 64 ? 64 : G);
-      if (!DVH_FV_BATCH || (int64_t)B * nvc < 1024) G = 0;
+      if ((int64_t)B * nvc < 1024) G = 0;
       if (const char* ev = getenv("DVH_FV_G")) G = atoi(ev);  // A/B: images per block (0: per-image kernel)
       if (G > 0) {
       dim3 grid(nvc, (B + G - 1) / G);
@@ -1246,7 +1205,7 @@ DVH_API int dvh_disp_fv_mfma(const double* FK, int32_t B, int32_t n_kb, int32_t 
   if ((int64_t)n_kb * n_fb > 8192) return set_error(-4, "FK grid larger than 8192 bins");
   if ((int64_t)nF * nV > 0x7fffffff) return set_error(-4, "f-v grid larger than 2^31 points");
   if (B <= 0 || nV <= 0) return 0;
-  constexpr int GI = DVH_FV_MF_GI;
+  constexpr int GI = kMfGI;
   const size_t lds = fv_mfma_lds(GI, n_kb * n_fb);
   hipError_t e = hipFuncSetAttribute((const void*)fv_mfma_kernel<GI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));

@@ -383,10 +383,19 @@ template <int NS>
 struct SosmMats {
   static constexpr int NST = 2 * NS;
   static constexpr int h = 0, Hm = kSmL, g = Hm + kSmL * NST, M = g + kSmL * NST, Mzi = M + NST * NST,
-                       MQ = Mzi + NST, MQ16 = MQ + NST * NST, size = MQ16 + NST * NST;
+                       MQ = Mzi + NST, MQ16 = MQ + NST * NST, Qk = MQ16 + NST * NST, size = Qk + 2;
 };
+// + the key (Q, Q16) the group transitions MQ / MQ16 were formed for: a scan whose own Q differs (a plan built for
+// another record length) uses a NaN transition, so that the mismatch shows in the output instead of a wrong filter
 constexpr int64_t sosm_plan_doubles(int n_sec) {
-  return kSmL + 2 * kSmL * (2 * n_sec) + 3 * (2 * n_sec) * (2 * n_sec) + 2 * n_sec;
+  return kSmL + 2 * kSmL * (2 * n_sec) + 3 * (2 * n_sec) * (2 * n_sec) + 2 * n_sec + 2;
+}
+// M^Q from the plan for a scan of group length Q: NaN when the plan's key is another Q
+template <int NS>
+__device__ __forceinline__ double sosm_mq(const double* __restrict__ mats, bool q16, int32_t Q, int idx) {
+  using O = SosmMats<NS>;
+  const double v = mats[(q16 ? O::MQ16 : O::MQ) + idx];
+  return mats[O::Qk + (q16 ? 1 : 0)] == (double)Q ? v : __builtin_nan("");
 }
 
 // Lanes e < NST: unit state e_e, zero input (Hm[:, e], M[:, e]); lane NST: zero state, unit sample (h, g).  Then
@@ -469,12 +478,13 @@ __global__ __launch_bounds__(512) void sosm_mats_kernel(const double* __restrict
     __syncthreads();
     if (act) mats[(pass == 0 ? O::MQ : O::MQ16) + e] = R[e];
   }
+  if (e < 2) mats[O::Qk + e] = (double)(e == 0 ? Q : Q16);
 }
 
 // sample i of row r of the forward pass's sequence: the odd extension of x (0 past n_ext)
 template <typename T>
 __device__ __forceinline__ double sosm_ext(const T* __restrict__ x, const SosGeom& G, int64_t r, int64_t i) {
-  if (i >= G.n_ext) return 0.0;
+  if (r >= G.n_rows || i >= G.n_ext) return 0.0;  // padding columns of a record's last tile: nothing to read
   const T* row = x + r * G.row_stride;
   const int64_t j = i - G.padlen;
   if (j >= 0 && j < G.n_t) return (double)row[j];
@@ -601,14 +611,16 @@ __device__ __forceinline__ void sosm_expand_x(const T* __restrict__ x, const Sos
       sosm_col(t, u, G.nb, r, k);
       const int64_t i = (int64_t)k * kSmL + lane, j = i - G.padlen;
       const double a = (double)raw.v[u];
-      double e;
-      if (j >= 0 && j < G.n_t)
-        e = a;
-      else if (j < 0)
-        e = r == rl ? 2.0 * xl - a : sosm_ext(x, G, r, i);
-      else
-        e = r == t.r0 ? 2.0 * xr - a : sosm_ext(x, G, r, i);
-      v[u] = (r < G.n_rows && i < G.n_ext) ? e : 0.0;
+      double e = 0.0;  // padding columns (r >= n_rows) and samples past the extension are zero, and read nothing
+      if (r < G.n_rows && i < G.n_ext) {
+        if (j >= 0 && j < G.n_t)
+          e = a;
+        else if (j < 0)
+          e = r == rl ? 2.0 * xl - a : sosm_ext(x, G, r, i);
+        else
+          e = r == t.r0 ? 2.0 * xr - a : sosm_ext(x, G, r, i);
+      }
+      v[u] = e;
     }
   }
 }
@@ -1015,9 +1027,6 @@ constexpr int kScanHW = 8, kScanPF = 16;
 __host__ __device__ constexpr int sosm_scan_q(int nb) { return nb > 2 ? (nb - 2 + kScanHW - 1) / kScanHW : 1; }
 // the 16-group scan on the matrix pipe (sosm_scanm_kernel): its group length, at most kScanMQ steps
 constexpr int kScanMG = 16, kScanMQ = 16;
-#ifndef DVH_SOS_SCANM
-#define DVH_SOS_SCANM 1  // the matrix-pipe scan where its 16 groups of <= 16 blocks cover the row (0: the VALU scans)
-#endif
 __host__ __device__ constexpr int sosm_scan_q16(int nb) { return nb > 2 ? (nb - 2 + kScanMG - 1) / kScanMG : 1; }
 
 template <int NS>
@@ -1095,7 +1104,7 @@ __global__ __launch_bounds__(32 * kScanHW, 4) void sosm_scan_kernel(SosGeom G, c
     double mq[NST];
 #pragma unroll
     for (int i = 0; i < NST; ++i) {
-      const double v = mats[O::MQ + jc * NST + i];
+      const double v = sosm_mq<NS>(mats, false, Q, jc * NST + i);
       mq[i] = act ? v : 0.0;
     }
     double c = act ? zlast[0][j] : 0.0;
@@ -1191,7 +1200,7 @@ __global__ __launch_bounds__(32 * kScanHW, 4) void sosm_scanr_kernel(SosGeom G, 
     double mq[NST];
 #pragma unroll
     for (int i = 0; i < NST; ++i) {
-      const double v = mats[O::MQ + jc * NST + i];
+      const double v = sosm_mq<NS>(mats, false, Q, jc * NST + i);
       mq[i] = act ? v : 0.0;
     }
     double c = act ? zf[(min(1 + Q, K) - 1) * NST + j] : 0.0;
@@ -1310,7 +1319,7 @@ __global__ __launch_bounds__(64, 1) void sosm_scanm_kernel(SosGeom G, const doub
   if (l < NST) {
     double mq[NST];
 #pragma unroll
-    for (int i = 0; i < NST; ++i) mq[i] = mats[O::MQ16 + l * NST + i];
+    for (int i = 0; i < NST; ++i) mq[i] = sosm_mq<NS>(mats, true, Q, l * NST + i);
     double cv = zl[0][l];
     carry[0][l] = cv;
     for (int g = 1; g + 1 < ng; ++g) {
@@ -1348,7 +1357,7 @@ __global__ __launch_bounds__(64, 1) void sosm_scanm_kernel(SosGeom G, const doub
 template <int NS>
 static void sosm_scan(const SosGeom& G, const double* plan, int Q, double* S, hipStream_t st) {
   if (G.nb <= 2) return;
-  if (DVH_SOS_SCANM && sosm_scan_q16(G.nb) <= kScanMQ)
+  if (sosm_scan_q16(G.nb) <= kScanMQ)  // the matrix-pipe scan where its 16 groups of <= 16 blocks cover the row
     hipLaunchKernelGGL(sosm_scanm_kernel<NS>, dim3((unsigned)G.n_rows), dim3(64), 0, st, G, plan,
                        (int32_t)sosm_scan_q16(G.nb), S);
   else if ((int64_t)(G.nb - 1) * 2 * NS <= kScanCap)
@@ -1486,10 +1495,6 @@ static int sosfiltfilt_blocks(T* x, const SosGeom& G, const double* sos, const d
   return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
 }
 
-#ifndef DVH_SOS_MFMA
-#define DVH_SOS_MFMA 1  // sosfiltfilt's block phases as float64 MFMA GEMMs (0: the VALU recursion per (row, block) lane)
-#endif
-
 // MFMA path (a plan given and the 32-bit column indices fit) or the VALU block recursion.  The block GEMMs add the
 // contributions of states that grow like 1 / (1 - r) for the filter's largest pole radius r, so their rounding grows
 // with it: relative error 1e-13 at r = 0.9956 (1.2-30 Hz at 250 Hz), 5e-10 at r = 0.99973 (0.08-1 Hz); callers
@@ -1497,7 +1502,7 @@ static int sosfiltfilt_blocks(T* x, const SosGeom& G, const double* sos, const d
 template <typename T>
 static int sosfiltfilt_dispatch(T* x, const SosGeom& Gm, const SosGeom& Gb, const double* sos, int n_sec, const double* zi,
                                 const double* plan, double* work, hipStream_t st) {
-  const bool mf = DVH_SOS_MFMA && plan && sosm_fits(Gm);
+  const bool mf = plan && sosm_fits(Gm);
   switch (n_sec) {
 #define DVH_SOS_CASE(n) \
   case n: return mf ? sosfiltfilt_mfma<T, n>(x, Gm, sos, zi, plan, work, st) : sosfiltfilt_blocks<T, n>(x, Gb, sos, zi, work, st);

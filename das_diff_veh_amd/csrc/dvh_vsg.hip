@@ -43,16 +43,10 @@ constexpr int kBlock = 512;  // sumsq kernel
 // EngF500 fits 4
 template <class E> struct Occ { static constexpr int v = 3; };
 template <> struct Occ<EngF500> { static constexpr int v = 4; };
-#ifndef DVH_DIRECT
-#define DVH_DIRECT 1  // fused-engine stack kernels: single-sided row tasks transformed across passes (direct_task)
-#endif
-#ifndef DVH_STACKF_OCC
-#define DVH_STACKF_OCC 0
-#endif
 // Occupancy target of the stack kernels: 4 waves/SIMD for the exact Stockham engines up to N = 500
 // (their spills at 128 VGPRs sit in the rare time-domain fallback only), else the engine default.
 template <class E> struct OccF {
-  static constexpr int v = DVH_STACKF_OCC ? DVH_STACKF_OCC : (E::kWaves == 4 && E::NFFT <= 500 ? 4 : Occ<E>::v);
+  static constexpr int v = E::kWaves == 4 && E::NFFT <= 500 ? 4 : Occ<E>::v;
 };
 
 // The engines with fused first / last stages (FusedOps: EngF500, EngP1024) take a per-pass pivot-slice
@@ -91,7 +85,7 @@ __device__ __forceinline__ bool engine_direct(E& eng, const VsgArgs& A, const fl
                                               const float* weight, int b, int e, int i, float2 (&Gh)[E::NH],
                                               bool* shared = nullptr) {
   if constexpr (Fused<E>::v) {
-    return DVH_DIRECT && eng.tab && eng.template direct_task<RAMP>(A, scales, order, weight, b, e, i, Gh, shared);
+    return eng.tab && eng.template direct_task<RAMP>(A, scales, order, weight, b, e, i, Gh, shared);
   } else {
     return false;
   }
@@ -122,12 +116,6 @@ __device__ __forceinline__ int pull_unit(uint32_t* counter, int lane) {
   return __builtin_amdgcn_readfirstlane(__shfl(u, 0));
 }
 
-#ifndef DVH_PULL_TASKS
-// validated launch: correlation waves pull row tasks from a counter instead of a static stride.  -1 (default):
-// the padded engines pull (w = 499: fused launch 4.80 -> 3.99 ms, their task costs vary with the pivot-slice
-// table's coverage), the exact ones keep the stride (synth10k / weights measured no better); 0 / 1: none / all
-#define DVH_PULL_TASKS -1
-#endif
 
 // XCD-aware block order (blocks are dealt round robin over the 8 XCDs, each with its own L2):
 // consecutive logical blocks -- the row tasks of one pass chunk, which all read that chunk's pivot
@@ -342,59 +330,6 @@ __global__ __launch_bounds__(64 * E::kWaves, Occ<E>::v) void vsg_gather_kernel(V
   }
 }
 
-// Stack mode: task = (chunk c, row i); the wave walks the chunk's passes (all of one class slot),
-// sums weight[p] * G_p in registers and adds the row into stack[slot] once.
-template <class E>
-__global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stack_kernel(VsgArgs A, const float* __restrict__ scales,
-                                                            const int32_t* __restrict__ order,
-                                                            const int32_t* __restrict__ chunk_tab, int32_t n_chunk,
-                                                            const float* __restrict__ weight,
-                                                            float* __restrict__ stack, const float2* __restrict__) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  E eng = make_engine<E>(lds);
-  bind_engine(eng, A, nullptr);
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  constexpr int NJ = E::NJ;
-  const int64_t n_task = (int64_t)n_chunk * A.R;
-  const int64_t stride = (int64_t)gridDim.x * E::kWaves;
-  for (int64_t t = (int64_t)xcd_block() * E::kWaves + wave; t < n_task; t += stride) {
-    const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
-    const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
-    // first pass of the wave's next task (for the cross-task slice prefetch)
-    int np = -1, ni = 0;
-    if (t + stride < n_task) {
-      const int c2 = uni((int)((t + stride) / A.R));
-      ni = uni((int)((t + stride) % A.R));
-      const int b2 = sld(chunk_tab + 3 * c2);
-      if (b2 < sld(chunk_tab + 3 * c2 + 1)) np = sld(order + b2);
-    }
-    float acc[NJ];
-#pragma unroll
-    for (int m = 0; m < NJ; ++m) acc[m] = 0.f;
-    RowTask task = b < e ? make_task(A, sld(order + b), i) : RowTask{};
-    for (int q = b; q < e; ++q) {
-      const int p = sld(order + q);
-      RowTask tn = task;
-      const bool has_next = (q + 1 < e) || np >= 0;
-      if (q + 1 < e) tn = make_task(A, sld(order + q + 1), i);
-      else if (np >= 0) tn = make_task(A, np, ni);
-      float G[NJ];
-      gather_row<E>(eng, A, scales, p, task, tn, has_next, lane, G);
-      const float wp = sld(weight + p);
-#pragma unroll
-      for (int m = 0; m < NJ; ++m) acc[m] += G[m] * wp;
-      task = tn;
-    }
-    float* o = stack + ((int64_t)slot * A.R + i) * A.w;
-#pragma unroll
-    for (int m = 0; m < NJ; ++m) {
-      const int j = lane + 64 * m;
-      if (j < A.w) atomicAdd(o + j, acc[m]);
-    }
-  }
-}
-
 // Stack mode, exact transforms (N == w): every pass's contribution is accumulated directly as the
 // spectrum of its output row, Ghat[m] += w_p (alpha f_f Phase_F(Cf) + beta f_o Phase_O(Co)), where
 // each lag convention of the reference is a conjugation and a phase ramp:
@@ -408,7 +343,7 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
                                              float* __restrict__ stack, int64_t t0, int64_t stride,
-                                             uint32_t* tq = nullptr, uint32_t* started = nullptr) {
+                                             uint32_t* tq = nullptr) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -423,7 +358,6 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
   int64_t tn = tq ? pull_unit(tq, lane_t) : t0;
   for (int64_t t = tn; t < n_task; t = tn) {
     tn = tq ? (int64_t)pull_unit(tq, lane_t) : t + stride;
-    if (started && lane_t == 0) atomicAdd(started, 1u);  // the scan's pacing (DVH_SCAN_PACE)
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
     int np = -1, ni = 0;
@@ -559,7 +493,7 @@ __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const flo
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
                                              float* __restrict__ stack, int64_t t0, int64_t stride,
-                                             uint32_t* tq = nullptr, uint32_t* started = nullptr) {
+                                             uint32_t* tq = nullptr) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -781,18 +715,9 @@ __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2*
 // its windows instead: scan_tab[s] = first record row of window s, and unit_scan[u] = the window whose
 // flag unit u takes, so a pass imaged at several pivots is validated once per launch.
 constexpr int kScanRows = 16;
-#ifndef DVH_SCAN_DEPTH
-#define DVH_SCAN_DEPTH 16
-#endif
-constexpr int kScanDepth = DVH_SCAN_DEPTH;  // 16-byte loads per lane in flight
-#ifndef DVH_SCAN_AUX
-#define DVH_SCAN_AUX 2
-#endif
-#ifndef DVH_SCAN_SLEEP
-#define DVH_SCAN_SLEEP 0
-#endif
-constexpr int kScanAux = DVH_SCAN_AUX;  // cache policy of the scan's buffer loads (nt; allocating loads measured 4 %
-                                        // slower on synth10k)
+constexpr int kScanDepth = 16;  // 16-byte loads per lane in flight (8 / 12 / 24 measured no better)
+constexpr int kScanAux = 2;     // cache policy of the scan's buffer loads (nt; allocating loads measured 4 % slower on
+                                // synth10k)
 
 __device__ __forceinline__ uint32_t absbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
 
@@ -824,9 +749,6 @@ __device__ __forceinline__ uint32_t scan_span(const float* __restrict__ q, int n
     off += 1024;
   }
   for (int s0 = 0; s0 < nsteps; s0 += D) {
-#if DVH_SCAN_SLEEP
-    __builtin_amdgcn_s_sleep(DVH_SCAN_SLEEP);  // A/B: a throttled stream (64 x N clocks per 16 KB of a wave)
-#endif
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const u32x4 v = r[d] & 0x7fffffffu;
@@ -861,20 +783,10 @@ struct ScanArgs {
 };
 
 // Pull scan units (window, kScanRows channel rows) until none is left; atomicMax into vflag[window].
-// Pacing (DVH_SCAN_PACE = L > 0, fused launches of the exact engines): the unit of window q waits until the correlation
-// has started the tasks of chunk q n_chunk / n_pass - L, so that the scan streams the windows the correlation is
-// loading instead of running ahead of it.
-#ifndef DVH_SCAN_PACE
-#define DVH_SCAN_PACE 0
-#endif
-struct ScanPace {
-  const uint32_t* started = nullptr;  // correlation tasks started
-  int64_t n_chunk = 0, n_pass = 1, R = 0;
-};
 template <int D = kScanDepth>
 __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, uint32_t* __restrict__ vflag,
                                            uint32_t* __restrict__ counter, int lane,
-                                           const int32_t* __restrict__ sorder = nullptr, ScanPace pace = ScanPace{}) {
+                                           const int32_t* __restrict__ sorder = nullptr) {
   const int upp = (S.n_ch + kScanRows - 1) / kScanRows;  // units per window
   const int n_units = S.n_win * upp;
   const bool vec = (S.n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
@@ -883,11 +795,6 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
   while (u < n_units) {
     const int un = pull_unit(counter, lane);  // the next unit's index, fetched under this unit's loads
     const int q = u / upp, c0 = (u - q * upp) * kScanRows;
-    if (pace.started) {
-      const int64_t need = min((q * pace.n_chunk / pace.n_pass - DVH_SCAN_PACE) * pace.R, pace.n_chunk * pace.R);
-      while ((int64_t)__hip_atomic_load(pace.started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
-        __builtin_amdgcn_s_sleep(4);
-    }
     const int s = (sorder && !S.tab) ? sld(sorder + q) : q;
     const float* base = S.tab ? A.win + (int64_t)sld(S.tab + s) * A.ch_stride : A.win + (int64_t)s * A.pass_stride;
     const uint32_t m = scan_rows<D>(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
@@ -896,135 +803,9 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
   }
 }
 
-// ---- scan skipping (DVH_SCAN_SKIP): the scan leaves out the 1 KB blocks of a gather row that lie wholly inside
-// the row's correlated slices -- [a + q hop, + w) over its nwin sub-windows on each side, loaded by the
-// correlation waves, which report a NaN / inf among them to the pass's flag (FusedOps::report).  Only for the
-// default windows (window = pass) of the fused engines.  A window whose flag ends at 0 (nothing non-zero in
-// the scanned part) is rescanned whole afterwards (window_zero_fixup_kernel), so all-zero windows stay exact.
-constexpr int kBlkF = 256;  // floats per scan block: one 16-byte load per lane
-#ifndef DVH_SKIP_DEPTH
-#define DVH_SKIP_DEPTH 12
-#endif
-constexpr int kSkipDepth = DVH_SKIP_DEPTH;  // 16-byte loads per lane in flight in the skipping scan
-
-// the gather row's skipped block ranges [s0, e0), [s1, e1) (blocks wholly inside a correlated slice)
-__device__ __forceinline__ void row_skip(const VsgArgs& A, int p, int i, int& s0, int& e0, int& s1, int& e1) {
-  s0 = e0 = s1 = e1 = 0;
-  if (i < 0 || i >= A.R) return;
-  const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
-  auto range = [&](int a, int L, int& s, int& e) {
-    const int nw = n_subwin(L, A.w, A.hop);
-    const int cov = nw > 0 ? (nw - 1) * A.hop + A.w : 0;
-    s = (a + kBlkF - 1) / kBlkF;
-    e = (a + cov) / kBlkF;
-    if (e <= s) s = e = 0;
-  };
-  range(sld(seg), sld(seg + 1), s0, e0);
-  if (A.flags & kFlagOtherSide) range(sld(seg + 2), sld(seg + 3), s1, e1);
-  if (s1 < s0) {  // ordered
-    int t = s0; s0 = s1; s1 = t;
-    t = e0; e0 = e1; e1 = t;
-  }
-  if (e0 > s1 && s1 < e1) {  // overlapping ranges merge
-    e0 = max(e0, e1);
-    s1 = e1 = 0;
-  }
-}
-
-// rows [c0, c1) of pass p's window (n_t samples each, ch_stride apart, 16-byte aligned rows): max |x| bit
-// pattern over the blocks the correlation does not load; kScanDepth 16-byte loads per lane in flight, the
-// cursor (row, block, skip ranges) advanced in scalar registers
-__device__ __forceinline__ uint32_t scan_rows_skip(const VsgArgs& A, const ScanArgs& S, int p, int c0, int c1, int lane) {
-  const float* base = A.win + (int64_t)p * A.pass_stride;
-  const int64_t wbytes = ((int64_t)(S.n_ch - 1) * A.ch_stride + S.n_t) * 4;
-  const __amdgpu_buffer_rsrc_t rs = scan_rsrc(base, (uint32_t)min<int64_t>(wbytes, 0xffffffffLL));
-  const int row0 = sld(A.pass_tab + 2 * p);
-  const int nblk = (S.n_t + kBlkF - 1) / kBlkF;
-  int c = c0, j = 0, s0, e0, s1, e1, ns0, ne0, ns1, ne1;
-  row_skip(A, p, c - row0, s0, e0, s1, e1);
-  row_skip(A, p, c + 1 - row0, ns0, ne0, ns1, ne1);  // the next row's ranges formed a row ahead
-  auto fix = [&]() {  // the cursor past the skipped ranges and onto the next row when a row is done
-    for (;;) {
-      if (j >= s0 && j < e0) j = e0;
-      if (j >= s1 && j < e1) j = e1;
-      if (j < nblk || c >= c1) return;
-      ++c;
-      j = 0;
-      s0 = ns0;
-      e0 = ne0;
-      s1 = ns1;
-      e1 = ne1;
-      if (c + 1 < c1) row_skip(A, p, c + 1 - row0, ns0, ne0, ns1, ne1);
-    }
-  };
-  fix();
-  const int lofs = lane * 16;
-  auto next = [&]() -> int {  // byte offset of this lane's 16 bytes of the cursor's block (out of range when done)
-    int off = -1;
-    if (c < c1) {
-      const int f = j * kBlkF + lane * 4;
-      off = f < S.n_t ? (int)(((int64_t)c * A.ch_stride + (int64_t)j * kBlkF) * 4) + lofs : -1;
-      ++j;
-      fix();
-    }
-    return off;
-  };
-  constexpr int D = kSkipDepth;
-  uint32_t m = 0;
-  u32x4 r[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, next(), 0, kScanAux);
-  while (c < c1) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const u32x4 v = r[d] & 0x7fffffffu;
-      m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
-      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, next(), 0, kScanAux);
-    }
-  }
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    const u32x4 v = r[d] & 0x7fffffffu;
-    m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
-  }
-  return wave_max_u32(m);
-}
-
-// scan_units with skipping (default windows only: window s = pass order[q])
-__device__ __forceinline__ void scan_units_skip(const VsgArgs& A, const ScanArgs& S, uint32_t* __restrict__ vflag,
-                                                uint32_t* __restrict__ counter, int lane,
-                                                const int32_t* __restrict__ sorder) {
-  const int upp = (S.n_ch + kScanRows - 1) / kScanRows;
-  const int n_units = S.n_win * upp;
-  int u = pull_unit(counter, lane);
-  while (u < n_units) {
-    const int un = pull_unit(counter, lane);
-    const int q = u / upp, c0 = (u - q * upp) * kScanRows;
-    const int s = sorder ? sld(sorder + q) : q;
-    const uint32_t m = scan_rows_skip(A, S, s, c0, min(c0 + kScanRows, S.n_ch), lane);
-    if (lane == 0) atomicMax(vflag + s, m);
-    u = un;
-  }
-}
-
-// Windows whose flag is still 0 after a skipping launch are rescanned whole (their scanned part was all zero;
-// the correlated slices may not be): one block per window, nothing to do for the usual non-zero flag.
-__global__ __launch_bounds__(256) void window_zero_fixup_kernel(VsgArgs A, ScanArgs S, uint32_t* __restrict__ vflag) {
-  const int s = blockIdx.x;
-  if (vflag[s] != 0) return;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const float* base = A.win + (int64_t)s * A.pass_stride;
-  uint32_t m = 0;
-  for (int c = wave; c < S.n_ch; c += 4)
-    for (int t = lane; t < S.n_t; t += 64) m = max(m, absbits(base[(int64_t)c * A.ch_stride + t]));
-  m = wave_max_u32(m);
-  if (lane == 0 && m) atomicMax(vflag + s, m);
-}
-
-#ifndef DVH_CORR_PRIO
-#define DVH_CORR_PRIO 2  // s_setprio of the correlation waves while they correlate (scan waves stay at 0): the
-                         // correlation is the critical path; 1 / 2 / 3 all measured 127.7 k -> 136 k windows/s on synth10k
-#endif
+// correlation waves raise their issue priority while they correlate (scan waves stay at 0): the correlation is the
+// critical path; 1 / 2 / 3 all measured 127.7 k -> 136 k windows/s on synth10k
+constexpr int kCorrPrio = 2;
 
 // The row tasks of a stack launch: frequency-domain stacking with the engine's exact (N = w) transforms, or
 // with a zero-padded one (stackp_tasks).
@@ -1032,8 +813,8 @@ template <class E, bool EXACT>
 __device__ __forceinline__ void stack_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                             const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                             int32_t n_chunk, const float* __restrict__ weight, float* __restrict__ stack,
-                                            int64_t t0, int64_t stride, uint32_t* tq, uint32_t* started = nullptr) {
-  if constexpr (EXACT) stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq, started);
+                                            int64_t t0, int64_t stride, uint32_t* tq) {
+  if constexpr (EXACT) stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq);
   else stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq);
 }
 
@@ -1049,34 +830,19 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
   E eng = make_engine<E>(lds);
   bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool skip = DVH_SCAN_SKIP && Fused<E>::v && !S.tab && S.n_t % 4 == 0 && A.ch_stride % 4 == 0 &&
-                    A.pass_stride % 4 == 0 && (reinterpret_cast<uintptr_t>(A.win) % 16 == 0);
-  if constexpr (Fused<E>::v) {
-    if (skip) eng.vflag = vflag;
-  }
-  constexpr bool kPull = DVH_PULL_TASKS < 0 ? !EXACT : DVH_PULL_TASKS != 0;
+  // the padded engines' correlation waves pull row tasks from a counter (w = 499: fused launch 4.80 -> 3.99 ms, their
+  // task costs vary with the pivot-slice table's coverage); the exact ones keep the static stride (pulled, synth10k /
+  // weights measured no better: balanced waves all join the scan at once at the end)
+  constexpr bool kPull = !EXACT;
   if (wave < kFft) {
-#if DVH_CORR_PRIO
-    __builtin_amdgcn_s_setprio(DVH_CORR_PRIO);  // correlation waves issue first when both are ready
-#endif
+    __builtin_amdgcn_s_setprio(kCorrPrio);  // correlation waves issue first when both are ready
     stack_tasks<E, EXACT>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
-                          (int64_t)gridDim.x * kFft, kPull ? counter + 1 : nullptr,
-                          (DVH_SCAN_PACE > 0 && EXACT && !kPull) ? counter + 1 : nullptr);
-#if DVH_CORR_PRIO
+                          (int64_t)gridDim.x * kFft, kPull ? counter + 1 : nullptr);
     __builtin_amdgcn_s_setprio(0);
-#endif
   }
   // the chunks cover order[0, end of the last chunk): scan in that order when it lists every pass
   const int32_t* sorder = (n_chunk > 0 && sld(chunk_tab + 3 * (n_chunk - 1) + 1) == A.n_pass) ? order : nullptr;
-  ScanPace pace;
-  if (DVH_SCAN_PACE > 0 && EXACT && !kPull && sorder && !S.tab && wave >= kFft) {  // scan waves only
-    pace.started = counter + 1;
-    pace.n_chunk = n_chunk;
-    pace.n_pass = A.n_pass;
-    pace.R = A.R;
-  }
-  if (skip) scan_units_skip(A, S, vflag, counter, lane, sorder);
-  else scan_units<kDepth>(A, S, vflag, counter, lane, sorder, pace);
+  scan_units<kDepth>(A, S, vflag, counter, lane, sorder);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
@@ -1172,15 +938,10 @@ struct VsgKernels {
   int waves;
 };
 
-#ifndef DVH_FREQ_STACK
-#define DVH_FREQ_STACK 1
-#endif
-
 template <class E, bool EXACT>
 VsgKernels vsg_kernels() {
   const void* st;
-  if constexpr (!DVH_FREQ_STACK) st = (const void*)vsg_stack_kernel<E>;
-  else if constexpr (EXACT) st = (const void*)vsg_stackf_kernel<E>;
+  if constexpr (EXACT) st = (const void*)vsg_stackf_kernel<E>;
   else st = (const void*)vsg_stackp_kernel<E>;
   return VsgKernels{(const void*)vsg_scales_kernel<E>, (const void*)vsg_gather_kernel<E>, st,
                     E::kBlockBytes + E::kWaves * E::kWaveBytes, E::kWaves};
@@ -1288,31 +1049,11 @@ static int cu_count() {
   return n;
 }
 
-#ifndef DVH_VSTACK_FFT
-#define DVH_VSTACK_FFT 7  // EngF500: correlation waves per block of the validated stack launch (2 blocks per CU)
-#endif
-#ifndef DVH_VSTACK_SCAN
-#define DVH_VSTACK_SCAN 1  // scan waves per block
-#endif
-#ifndef DVH_VSTACK_BPC
-#define DVH_VSTACK_BPC 2  // blocks per CU
-#endif
-#ifndef DVH_VSTACK_OCC
-#define DVH_VSTACK_OCC 4  // EngF500 validated launch: waves per SIMD the registers are sized for (launch bounds)
-#endif
-#ifndef DVH_P1024_FFT
-#define DVH_P1024_FFT 7  // EngP1024 validated launch: correlation waves per block (one block per CU: LDS, registers)
-#endif
-#ifndef DVH_P1024_SCAN
-#define DVH_P1024_SCAN 1  // ... scan waves per block
-#endif
-#ifndef DVH_P1024_DEPTH
-#define DVH_P1024_DEPTH 32  // ... 16-byte loads per lane its scan waves keep in flight (their registers allow it: w = 499
-                            // synth10k launch 14.70 vs 15.08 ms at 16, 14.92 at 48; weights 1.84 vs 1.82 ms)
-#endif
-#ifndef DVH_PIVOT_TABLE
-#define DVH_PIVOT_TABLE 1  // stack launches at w = 500 with the per-pass pivot-slice spectra table
-#endif
+// Validated launch shapes.  EngF500: blocks of 7 correlation + 1 scan waves, 2 blocks per CU (4 waves per SIMD, the
+// registers sized for it by the launch bounds).  EngP1024: 7 + 1 waves, one block per CU (LDS, registers), its scan
+// waves keeping 32 loads per lane in flight (w = 499 synth10k launch 14.70 vs 15.08 ms at 16, 14.92 at 48).
+constexpr int kVsFft = 7, kVsScan = 1, kVsBpc = 2, kVsOcc = 4;
+constexpr int kP1Fft = 7, kP1Scan = 1, kP1Depth = 32;
 
 // The fused (correlation + validity scan) launch of each transform length: kernel, correlation / scan waves per
 // block, blocks per CU, LDS per block.
@@ -1327,15 +1068,15 @@ static VStack vstack(int bpc) {
 }
 static bool get_vstack(int n, VStack* v) {
   switch (n) {
-    case 500: *v = vstack<EngF500, DVH_VSTACK_FFT, DVH_VSTACK_SCAN, DVH_VSTACK_OCC, true>(DVH_VSTACK_BPC); return true;
+    case 500: *v = vstack<EngF500, kVsFft, kVsScan, kVsOcc, true>(kVsBpc); return true;
     case 512: *v = vstack<EngStockham<512, true>, 7, 1, 2, false>(1); return true;
-    case 1024: *v = vstack<EngP1024, DVH_P1024_FFT, DVH_P1024_SCAN, 2, false, DVH_P1024_DEPTH>(1); return true;
+    case 1024: *v = vstack<EngP1024, kP1Fft, kP1Scan, 2, false, kP1Depth>(1); return true;
     default: return false;
   }
 }
 
 // Transform lengths whose engine takes the pivot-slice table: 500 (EngF500) and the padded 1 024 (EngP1024).
-static bool table_engine(int n) { return DVH_PIVOT_TABLE && DVH_FREQ_STACK && (n == 500 || n == 1024); }
+static bool table_engine(int n) { return n == 500 || n == 1024; }
 
 template <class E>
 static int64_t table_bytes(int64_t n_pass) {
@@ -1388,15 +1129,11 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
     if (int rc = launch_table(A, n, tab, s)) return rc;
   const int64_t tasks = (int64_t)n_chunk * R;
   VStack v{};
-  if (DVH_FREQ_STACK && get_vstack(n, &v)) {
+  if (get_vstack(n, &v)) {
     const int64_t need = (tasks + v.fft - 1) / v.fft;
     const int grid = (int)(need < v.bpc * cu_count() ? (need > 0 ? need : 1) : v.bpc * cu_count());
     void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &tab};
     if (int rc = launch(v.fn, grid, v.fft + v.scan, v.lds, args, s)) return rc;
-    if (DVH_SCAN_SKIP && !scan_tab && S.n_win > 0) {  // the windows the skipping scan saw as all zero, rescanned whole
-      hipLaunchKernelGGL(window_zero_fixup_kernel, dim3((unsigned)S.n_win), dim3(256), 0, s, A, S, vflag);
-      if ((e = hipGetLastError()) != hipSuccess) return set_error(-3, hipGetErrorString(e));
-    }
   } else {  // no fused form: the scan as its own launch, then the plain stack launch
     void* sargs[] = {&A, (void*)&S, &vflag, &counter};
     if (int rc = launch((const void*)window_scan_kernel, 4 * cu_count(), 4, 0, sargs, s)) return rc;

@@ -11,90 +11,25 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#ifndef DVH_NO_READ2
-#define DVH_NO_READ2 0
-#endif
-// One LDS complex read.  With DVH_NO_READ2 the index is made opaque so that the compiler cannot
-// pair reads into ds_read2_b64 (8 LDS cycles on gfx950 against 2 + 2 for two ds_read_b64); measured
-// slower on the stack kernels (synth10k launch 3.84 vs 3.62-3.73 ms, sliding 9.65 vs 9.22 ms), so off.
-__device__ __forceinline__ float2 lds_ld(const float2* p, int idx) {
-#if DVH_NO_READ2
-  asm volatile("" : "+v"(idx));
-#endif
-  return p[idx];
-}
-
-#ifndef DVH_STAGE_UNROLL
-#define DVH_STAGE_UNROLL 1
-#endif
-#ifndef DVH_TW_RECUR
-#define DVH_TW_RECUR 1
-#endif
+// One LDS complex read (the compiler pairs neighbouring ones into ds_read2_b64; single reads measured slower on the
+// stack kernels despite the LDS cycles they save: their address arithmetic costs more).
+__device__ __forceinline__ float2 lds_ld(const float2* p, int idx) { return p[idx]; }
 
 namespace dvh {
 
-typedef float pk2 __attribute__((ext_vector_type(2)));
-#ifndef DVH_PK_BFLY
-#define DVH_PK_BFLY 0  // 1: butterfly adds / constant multiplies as packed f32 vector ops (v_pk_*_f32)
-#endif
-#if DVH_PK_BFLY
-__device__ __forceinline__ pk2 vp(float2 a) { return __builtin_bit_cast(pk2, a); }
-__device__ __forceinline__ float2 fp(pk2 a) { return __builtin_bit_cast(float2, a); }
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return fp(vp(a) + vp(b)); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return fp(vp(a) - vp(b)); }
-#else
+// Complex arithmetic as plain f32 ops (packed v_pk_*_f32 forms measured no faster on gfx950).
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-#endif
-#ifndef DVH_PK_CMUL
-#define DVH_PK_CMUL 0
-#endif
-// a * b.  Default (0): plain C.  1: two packed ops (v_pk_mul_f32, then v_pk_fma_f32 with operand
-// selects / negation); 2: four scalar ops in asm.  Measured on the N = 500 stack kernel: packed
-// forms are no faster than scalar FMAs on gfx950 (1 was 2-3 % slower), so the default stays C.
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-#if DVH_PK_CMUL == 1
-  const pk2 av = {a.x, a.y}, bv = {b.x, b.y};
-  pk2 t, r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(av), "v"(bv));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(av), "v"(bv), "v"(t));
-  return make_float2(r.x, r.y);
-#elif DVH_PK_CMUL == 2
-  float re, im;  // four scalar VALU ops (kept out of packed form)
-  asm("v_mul_f32 %0, %1, %2" : "=v"(re) : "v"(a.y), "v"(b.y));
-  asm("v_fma_f32 %0, %1, %2, -%3" : "=v"(re) : "v"(a.x), "v"(b.x), "v"(re));
-  asm("v_mul_f32 %0, %1, %2" : "=v"(im) : "v"(a.y), "v"(b.x));
-  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(im) : "v"(a.x), "v"(b.y), "v"(im));
-  return make_float2(re, im);
-#else
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-#endif
 }
-#if DVH_PK_BFLY
-__device__ __forceinline__ float2 cscale(float2 a, float s) { return fp(vp(a) * s); }
-#else
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
-#endif
 // -i * a and +i * a
 __device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
 __device__ __forceinline__ float2 mul_pi(float2 a) { return make_float2(-a.y, a.x); }
 // m + (-i) u = (m.x + u.y, m.y - u.x) and m + i u = (m.x - u.y, m.y + u.x)
-#if DVH_PK_BFLY
-// one v_pk_add_f32 each: the swap and the negation ride on op_sel / neg modifiers
-__device__ __forceinline__ float2 add_mi(float2 m, float2 u) {
-  pk2 r;
-  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(vp(m)), "v"(vp(u)));
-  return fp(r);
-}
-__device__ __forceinline__ float2 add_pi(float2 m, float2 u) {
-  pk2 r;
-  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(vp(m)), "v"(vp(u)));
-  return fp(r);
-}
-#else
 __device__ __forceinline__ float2 add_mi(float2 m, float2 u) { return cadd(m, mul_mi(u)); }
 __device__ __forceinline__ float2 add_pi(float2 m, float2 u) { return cadd(m, mul_pi(u)); }
-#endif
 
 // Orders this wave's LDS accesses across lanes (a single wave executes LDS ops in order; the
 // fences stop the compiler from moving loads/stores across the stage boundary).
@@ -144,17 +79,10 @@ template <> struct Dft<5> {
     constexpr float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
     const float2 t1 = cadd(a[1], a[4]), t2 = cadd(a[2], a[3]);
     const float2 t3 = csub(a[1], a[4]), t4 = csub(a[2], a[3]);
-#if DVH_PK_BFLY
-    const float2 m1 = fp(vp(a[0]) + c1 * vp(t1) + c2 * vp(t2));
-    const float2 m2 = fp(vp(a[0]) + c2 * vp(t1) + c1 * vp(t2));
-    const float2 u1 = fp(s1 * vp(t3) + s2 * vp(t4));
-    const float2 u2 = fp(s2 * vp(t3) - s1 * vp(t4));
-#else
     const float2 m1 = make_float2(a[0].x + c1 * t1.x + c2 * t2.x, a[0].y + c1 * t1.y + c2 * t2.y);
     const float2 m2 = make_float2(a[0].x + c2 * t1.x + c1 * t2.x, a[0].y + c2 * t1.y + c1 * t2.y);
     const float2 u1 = make_float2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y);
     const float2 u2 = make_float2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y);
-#endif
     a[0] = cadd(a[0], cadd(t1, t2));
     a[1] = add_mi(m1, u1);
     a[4] = add_pi(m1, u1);
@@ -162,26 +90,6 @@ template <> struct Dft<5> {
     a[3] = add_pi(m2, u2);
   }
 };
-
-// Swizzled LDS layout (SW = 1, the padded 1 024-point engine): element n lives at n ^ (((n >> 4) & 3) << 2), i.e.
-// bits 4-5 of the index are XORed into bits 2-3.  Radix-4 stages write out[(i - k) R + k + q Ls]: at Ls = 4 a
-// 16-lane store group (ds_write_b64, 32 banks = 16 complex slots) spans four 128-byte rows at the same bank offset
-// (a 4-way conflict in the plain layout); the swizzle spreads the four rows over distinct bank quarters.  Contiguous
-// reads stay conflict-free (the map permutes bits 0-4 within every aligned run of 32), and bits >= 6 are untouched,
-// so offsets that are multiples of 64 commute with it.
-// SW bit 0: the swizzled layout; bit 1: the contiguous stage twiddles (below).
-template <int SW>
-__device__ __forceinline__ int lds_idx(int n) {
-  return (SW & 1) ? (n ^ (((n >> 4) & 3) << 2)) : n;
-}
-// With SW bit 1, the stage twiddles w1 = tw[k (N / (Ls R))] of the stages with 4 <= Ls and a table stride > 1 are also
-// held contiguously in k after the main table (tw[N + (Ls - 4) / 3 + k], Ls = 4, 16, 64, N <= 1024;
-// tw_entries<N, 1>): a strided read of the main table puts up to 16 distinct addresses of a lane group on one or
-// two banks.
-template <int N, int SW>
-constexpr int tw_entries() {
-  return SW ? N + (N > 16 ? 4 : 0) + (N > 64 ? 16 : 0) + (N > 256 ? 64 : 0) : N;  // stages Ls < N / 4
-}
 
 // 16-point DFT in registers, natural order in and out (4 x 4: radix-4 DFTs over t2 of a[t1 + 4 t2], twiddles
 // W16^(t1 q2), radix-4 DFTs over t1 into a[q2 + 4 q1]).  HALF: only a[0..7] are non-zero (a zero-padded input).
@@ -240,47 +148,40 @@ __device__ __forceinline__ void twiddle16(float2 (&a)[16], float2 w1, float2 w4,
   }
 }
 
-template <int N, int Ls, int R, int SW = 0>
+template <int N, int Ls, int R>
 __device__ __forceinline__ void stockham_stage(const float2* __restrict__ in, float2* __restrict__ out,
                                                const float2* __restrict__ tw, int lane) {
   constexpr int NB = N / R;
   constexpr int TWS = N / (Ls * R);
   static_assert(N % (Ls * R) == 0, "plan does not divide N");
-  static_assert(!SW || (R == 4 && NB % 64 == 0 && N <= 1024 && (TWS == 1 || Ls == 4 || Ls == 16 || Ls == 64)),
-                "the swizzled layout is for power-of-4 stages whose reads are 64-aligned runs");
   auto round = [&](int i0) {
     const int i = i0 + lane;
     if (NB % 64 == 0 || i < NB) {
       const int k = i % Ls;
       float2 a[R];
-      const int ib = lds_idx<SW>(i);  // + t NB: NB is a multiple of 64 when SW
 #pragma unroll
-      for (int t = 0; t < R; ++t) a[t] = lds_ld(in, ib + t * NB);
+      for (int t = 0; t < R; ++t) a[t] = lds_ld(in, i + t * NB);
       if (Ls > 1) {
-#if DVH_TW_RECUR
-        // one table read per butterfly, powers by recurrence (LDS reads are the scarcer resource)
-        const float2 w1 = ((SW & 2) && TWS > 1) ? tw[N + (Ls - 4) / 3 + k] : tw[k * TWS];
+        // one table read per butterfly, powers by recurrence (LDS reads are the scarcer resource; per-power table
+        // reads measured 8 % slower)
+        const float2 w1 = tw[k * TWS];
         float2 wt = w1;
 #pragma unroll
         for (int t = 1; t < R; ++t) {
           a[t] = cmul(a[t], wt);
           if (t + 1 < R) wt = cmul(wt, w1);
         }
-#else
-#pragma unroll
-        for (int t = 1; t < R; ++t) a[t] = cmul(a[t], tw[t * k * TWS]);
-#endif
       }
       Dft<R>::run(a);
       const int base = (i - k) * R + k;
 #pragma unroll
-      for (int q = 0; q < R; ++q) out[lds_idx<SW>(base + q * Ls)] = a[q];
+      for (int q = 0; q < R; ++q) out[base + q * Ls] = a[q];
     }
   };
   // Short radix <= 5 stages (<= 2 rounds of 64 butterflies) are unrolled so that the second round's LDS reads
   // overlap the first round's arithmetic (measured -8 % on the N = 500 stack kernel); long ones stay
   // rolled (code size, registers).
-  if constexpr (DVH_STAGE_UNROLL && NB <= 128 && R <= 5) {
+  if constexpr (NB <= 128 && R <= 5) {
 #pragma unroll
     for (int i0 = 0; i0 < NB; i0 += 64) round(i0);
   } else {
@@ -314,19 +215,13 @@ template <> struct FftPlan<512> { using T = Stockham<512, 1, 4, 4, 4, 4, 2>; };
 template <> struct FftPlan<1024> { using T = Stockham<1024, 1, 4, 4, 4, 4, 4>; };
 template <> struct FftPlan<2048> { using T = Stockham<2048, 1, 4, 4, 4, 4, 4, 2>; };
 
-// Block-cooperative twiddle table tw[m] = exp(-2*pi*i*m/N), computed in double then rounded; with SW also the
-// contiguous stage tables of stockham_stage<..., SW & 2> (the same values: entry (Ls, k) is tw[k N / (4 Ls)]).
-template <int N, int SW = 0>
+// Block-cooperative twiddle table tw[m] = exp(-2*pi*i*m/N), computed in double then rounded.
+template <int N>
 __device__ __forceinline__ void init_twiddles(float2* tw) {
-  for (int e = threadIdx.x; e < tw_entries<N, SW>(); e += blockDim.x) {
-    int m = e;
-    if (e >= N) {  // stage table entry: Ls = 4, 16, 64 at offsets 0, 4, 20
-      const int o = e - N, Ls = o < 4 ? 4 : (o < 20 ? 16 : 64), k = o - (Ls - 4) / 3;
-      m = k * (N / (4 * Ls));
-    }
+  for (int m = threadIdx.x; m < N; m += blockDim.x) {
     double s, c;
     sincospi(2.0 * (double)m / (double)N, &s, &c);
-    tw[e] = make_float2((float)c, (float)(-s));
+    tw[m] = make_float2((float)c, (float)(-s));
   }
 }
 

@@ -112,20 +112,8 @@ __device__ __forceinline__ int opaque(int v) {
 
 // |x| != 0 as a bit mask (NaN included); OR-accumulate, test once per sub-window
 __device__ __forceinline__ uint32_t nzbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
-#ifndef DVH_SCAN_SKIP
-#define DVH_SCAN_SKIP 0  // validated launch: the scan skips the correlated slices, which the correlation validates
-#endif
-// With scan skipping the fused engines accumulate max |x| bit patterns (!= 0 is the same non-zero test, and
-// >= 0x7f800000 flags a NaN / inf among the loaded samples, the validity of the bytes the scan leaves out);
-// otherwise the OR (one v_and_or per sample against an and + max).
-__device__ __forceinline__ uint32_t maxbits(uint32_t b, float x) {
-#if DVH_SCAN_SKIP
-  return max(b, nzbits(x));
-#else
-  return b | nzbits(x);
-#endif
-}
-constexpr uint32_t kInfBits = 0x7f800000u;
+// OR-accumulated non-zero bits of the loaded samples (one v_and_or per sample)
+__device__ __forceinline__ uint32_t maxbits(uint32_t b, float x) { return b | nzbits(x); }
 
 __device__ __forceinline__ void accumulate_cross(float2 Az, float2 Bc, float2& C) {
   // P = (A + B) / 2, R = (A - B) / 2i with B = conj(Bc)  ->  P conj(R) = (i / 4) (A + B) conj(A - B)
@@ -333,7 +321,6 @@ struct FusedOps {
   bool live_f, live_o;
   const float2* tab = nullptr;  // the pass table of pivot spectra (stack kernels), or none
   int w;                        // sub-window length: the padded engines load samples n < w
-  uint32_t* vflag = nullptr;    // validated launch with scan skipping: per-pass flags the loads report NaN / inf to
 
   __device__ FusedOps(char* lds, int wave, int lane_, int w_) : lane(lane_), live_f(false), live_o(false), w(w_) {
     tw = reinterpret_cast<float2*>(lds);
@@ -348,11 +335,6 @@ struct FusedOps {
   // the stages after stage 1 of the transform whose stage-1 output is in bufB; cross spectra into C
   __device__ __forceinline__ void finish(float2 (&C)[kNH]) const {
     self().finish_with([&](int j, float2 a, float2 b) { accumulate_cross(a, b, C[j]); });
-  }
-
-  // a NaN / inf among the samples this wave loaded for pass p (max |x| bits vm) -> the pass's validity flag
-  __device__ __forceinline__ void report(int p, uint32_t vm) const {
-    if (DVH_SCAN_SKIP && vflag && __ballot(vm >= kInfBits) != 0 && lane == 0) atomicMax(vflag + p, kInfBits);
   }
 
   // the pass's table entries hold all its sub-windows (head nwin of entry 0 >= 0)
@@ -373,7 +355,6 @@ struct FusedOps {
     live_f = live_o = false;
     auto start = [&](int q) { return q < t.nwin_f ? t.a_f + q * hop : t.a_o + (q - t.nwin_f) * hop; };
     float2 z[kNJ];
-    uint32_t vm = 0;
     if (nq > 0) load(t, start(0), z);
     for (int q = 0; q < nq; ++q) {
       uint32_t bp = 0, br = 0;
@@ -382,7 +363,6 @@ struct FusedOps {
         bp = maxbits(bp, z[j].x);
         br = maxbits(br, z[j].y);
       }
-      if (DVH_SCAN_SKIP) vm = max(vm, max(bp, br));
       const bool live = (__ballot(bp != 0) != 0) && (__ballot(br != 0) != 0);
       if (live) self().stage1(z);
       if (q + 1 < nq) load(t, start(q + 1), z);
@@ -395,7 +375,6 @@ struct FusedOps {
         finish(Co);
       }
     }
-    report(t.p, vm);
   }
 
   // ---- spectra_tab: the sub-windows whose pivot slices the table holds cost only their receivers ----
@@ -453,7 +432,6 @@ struct FusedOps {
     const TabJobs J = tab_jobs(t, head);
     const int nj = J.npair + J.nt;
     float2 z[kNJ];
-    uint32_t vm = 0;
     if (nj > 0) tab_load(t, J, 0, hop, z);
     for (int k = 0; k < nj; ++k) {
       const bool pairjob = k < J.npair;
@@ -463,7 +441,6 @@ struct FusedOps {
         bp = maxbits(bp, z[j].x);
         br = maxbits(br, z[j].y);
       }
-      if (DVH_SCAN_SKIP) vm = max(vm, max(bp, br));
       const bool nzp = __ballot(bp != 0) != 0, nzr = __ballot(br != 0) != 0;
       int s0 = 0, q0 = 0, a0 = 0, s1 = 0, q1 = 0, a1 = 0;
       bool la = false, lb = false;
@@ -524,7 +501,6 @@ struct FusedOps {
         finish(Co);
       }
     }
-    report(t.p, vm);
   }
 
   // ---- direct_task: a row task whose passes have only a table-served forward side ----
@@ -622,10 +598,6 @@ struct FusedOps {
         bp = maxbits(bp, z[j].x);
         br = maxbits(br, z[j].y);
       }
-      if (DVH_SCAN_SKIP) {  // each half's samples belong to its own pass: halves 2 jb, 2 jb + 1 of W per pass
-        report(__builtin_amdgcn_readlane(p, (2 * jb) / W), bp);
-        if (hb) report(__builtin_amdgcn_readlane(p, (2 * jb + 1) / W), br);
-      }
       // a receiver slice or its pivot slice identically zero: exactly zero in the reference
       const bool la = (__ballot(bp != 0) != 0) && sld(&Pa[BINS - 1].x) != 0.f;
       const bool lb = hb && (__ballot(br != 0) != 0) && sld(&Pb[BINS - 1].x) != 0.f;
@@ -700,10 +672,6 @@ struct FusedOps {
 //     five bins in registers -- no LDS write of the spectrum and no partner reads.
 // Half-spectrum slots per lane l: j < 3 -> f = l + 100 j (l <= 50); j = 3, 4 -> f = 100 - l + 100 (j - 3)
 // (1 <= l <= 49): each of the 251 bins f <= 250 exactly once.
-#ifndef DVH_S1_SWIZZLE
-#define DVH_S1_SWIZZLE 1
-#endif
-
 struct EngF500 : FusedOps<EngF500, 8, 5> {
   static constexpr int N = 500;
   static constexpr int NFFT = 500;
@@ -749,7 +717,6 @@ struct EngF500 : FusedOps<EngF500, 8, 5> {
       if (r == 0 || i < 125) {
         float2 a[4] = {z[4 * r], z[4 * r + 1], z[4 * r + 2], z[4 * r + 3]};
         Dft<4>::run(a);
-#if DVH_S1_SWIZZLE
         // the four outputs are two 16-byte stores, X[4i..4i+1] and X[4i+2..4i+3]; with both in that order an
         // 8-lane store group hits banks 8i mod 32 twice (2-way conflict, the engine's only one).  Lanes with
         // i & 4 store their second pair first, so each store's eight 16-byte pieces tile the 32 banks.
@@ -758,10 +725,6 @@ struct EngF500 : FusedOps<EngF500, 8, 5> {
         float4* d = reinterpret_cast<float4*>(bufB + 4 * i);
         d[o >> 1] = sw ? make_float4(a[2].x, a[2].y, a[3].x, a[3].y) : make_float4(a[0].x, a[0].y, a[1].x, a[1].y);
         d[(2 - o) >> 1] = sw ? make_float4(a[0].x, a[0].y, a[1].x, a[1].y) : make_float4(a[2].x, a[2].y, a[3].x, a[3].y);
-#else
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bufB[4 * i + q] = a[q];
-#endif
       }
     }
   }
@@ -834,33 +797,27 @@ struct EngF500 : FusedOps<EngF500, 8, 5> {
 
 
 // ------------------------------------------------------------------------------------------------
-// EngP1024: zero-padded N = 1024 radix-4 Stockham for the window lengths without an exact engine, w <= 512
-// (w = int(wlen / dt) = 499 at the reference's other operating point, dt = 0.004000000000001336): the linear
-// correlation of the zero-padded sub-windows (N >= 2w - 1) is folded back to the circular one in c().  The
-// transform is fused like EngF500's:
-//   stage 1 (radix 4, span 1) from the prefetched samples: butterfly i = lane + 64 r (r < 4) has inputs
-//     x[i + 256 t], of which only t < 2 can be non-zero (n < w <= 512), so a lane holds z[j] = x[lane + 64 j],
-//     j < 8 (half the registers of a 1 024-sample stage) and the butterflies drop their zero inputs;
-//   stages 2-4 (spans 4, 16, 64) through LDS;
-//   stage 5 (span 256) runs butterflies k and 256 - k in one lane -- round A: (l, 256 - l) for l >= 1 and
-//     (0, 128) on lane 0, both self-partnered; round B: (64 + l, 192 - l) -- so each lane holds X[f] and
-//     X[N - f] of its bins and forms their cross spectra in registers.
+// EngP1024: zero-padded N = 1024 Stockham for the window lengths without an exact engine, w <= 512 (w = int(wlen /
+// dt) = 499 at the reference's other operating point, dt = 0.004000000000001336): the linear correlation of the
+// zero-padded sub-windows (N >= 2w - 1) is folded back to the circular one in c().  The transform is fused like
+// EngF500's:
+//   the first stage from the prefetched samples: a lane holds z[j] = x[lane + 64 j], j < 8 (only samples n < w <=
+//     512 can be non-zero: half the registers of a 1 024-sample stage), and its butterflies drop the zero inputs;
+//   the last stage (radix 4, span 256) runs butterflies k and 256 - k in one lane -- round A: (l, 256 - l) for l >= 1
+//     and (0, 128) on lane 0, both self-partnered; round B: (64 + l, 192 - l) -- so each lane holds X[f] and X[N - f]
+//     of its bins and forms their cross spectra in registers.
 // Half-spectrum slots per lane l (each bin f <= 512 exactly once):
 //   j = 0, 1: l, l + 256;  j = 2, 3: 256 - l, 512 - l (lane 0: 128, 384);  j = 4..7: 64 + l, 320 + l, 192 - l,
 //   448 - l;  j = 8: 512 (lane 0 only).
-#ifndef DVH_P1024_R16
-#define DVH_P1024_R16 1  // 1: the transforms as 16 x 16 x 4 (forward) and 4 x 16 x 16 (inverse) radix stages (below)
-#endif
-#ifndef DVH_P1024_SW
-#define DVH_P1024_SW 2  // EngP1024's LDS layout / twiddles (stockham_stage SW bits): 2 = contiguous stage twiddles,
-                        // 3 = also the XOR-swizzled layout (conflict-free stores, but its per-store address XORs cost
-                        // more VALU than the conflicts: w = 499 synth10k launch 16.1 vs 15.65 ms)
-#endif
-#ifndef DVH_P1024_R16TW
-#define DVH_P1024_R16TW 1  // radix-16 stage twiddles from contiguous per-stage tables (0: strided reads of the main table)
-#endif
+// The transforms run as radix-16 stages: forward = radix 16 (span 1, from the registers, zero-padded half) -> LDS A ->
+// radix 16 (span 16) -> LDS B -> the paired radix-4 last stage (span 256) in registers; inverse = radix 4 (span 1,
+// from the registers) -> LDS B -> radix 16 (span 4) -> LDS A -> radix 16 (span 64) -> Y in LDS B.  Two LDS round trips
+// per transform instead of four radix-4 ones, one wave synchronisation per stage boundary, and the twiddle products of
+// two radix-4 stages merged into one radix-16 stage.  Buffer A is padded (the span-1 forward stage's 16 outputs per
+// lane at n + n / 16, the span-4 inverse stage's at n + 4 (n / 64)), so the stores and reads of every stage are
+// conflict free; buffer B is plain.  (An XOR-swizzled radix-4 layout cut the conflicts further but cost 25 % more VALU
+// for no gain)
 struct EngP1024 : FusedOps<EngP1024, 8, 9> {
-  static constexpr int SW = DVH_P1024_SW;
   static constexpr int N = 1024;
   static constexpr int NFFT = 1024;
   static constexpr int NJ = 8;  // sample registers: n < N / 2
@@ -868,32 +825,21 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   static constexpr int kWaves = 4;
   static constexpr bool kNextTask = false;
   static constexpr int kTabBins = 520;  // bins f <= 512; [519].x: the slice's non-zero flag
-  // LDS layout (lds_idx<SW>) of both buffers and the twiddle table with its contiguous stage tables (conflict-free
-  // twiddle reads; with SW & 1 also conflict-free stage stores: the round-4 build spent 2.9 bank-conflict cycles per
-  // LDS instruction on the Ls = 4 stores and the strided twiddle reads)
-  // Radix-16 form (DVH_P1024_R16): forward = radix 16 (span 1, from the registers, zero-padded half) -> LDS A ->
-  // radix 16 (span 16) -> LDS B -> the paired radix-4 last stage (span 256) in registers; inverse = radix 4 (span 1,
-  // from the registers) -> LDS B -> radix 16 (span 4) -> LDS A -> radix 16 (span 64) -> Y in LDS B.  Two LDS round
-  // trips per transform instead of four, one wave synchronisation per stage boundary, and the twiddle products of two
-  // radix-4 stages merged into one radix-16 stage.  Buffer A is padded (the span-1 forward stage's 16 outputs per lane
-  // at n + n / 16, the span-4 inverse stage's at n + 4 (n / 64)), so the stores and reads of every stage are conflict
-  // free; buffer B is plain.
-  static constexpr bool R16 = DVH_P1024_R16 != 0;
-  static constexpr int kBufA = R16 ? N + N / 16 : N;
-  static constexpr size_t kWaveBytes = sizeof(float2) * (kBufA + N);         // buffers A and B
-  // Radix-16 stage twiddles, contiguous per stage after the tables above: stage Ls holds w^k, w^4k, w^8k (w = e^(-2 pi
+  static constexpr int kBufA = N + N / 16;
+  static constexpr size_t kWaveBytes = sizeof(float2) * (kBufA + N);  // buffers A and B
+  // Radix-16 stage twiddles, contiguous per stage after the main table: stage Ls holds w^k, w^4k, w^8k (w = e^(-2 pi
   // i Ls' / N), Ls' = N / (16 Ls)) for k < Ls at r16_tw(Ls) + {0, Ls, 2 Ls} + k, so that a stage's reads by lanes of
   // consecutive k are consecutive (read from the main table at stride 4 k, 16 k, 32 k they cost 1.6 bank-conflict
   // cycles per LDS instruction of the whole launch).
-  static constexpr int kR16Tw = tw_entries<N, SW>();
-  static constexpr int kR16TwEntries = R16 ? 3 * (16 + 4 + 64) : 0;
+  static constexpr int kR16Tw = N;
+  static constexpr int kR16TwEntries = 3 * (16 + 4 + 64);
   static constexpr int r16_tw(int Ls) { return kR16Tw + (Ls == 16 ? 0 : (Ls == 4 ? 48 : 60)); }
-  static constexpr size_t kBlockBytes = sizeof(float2) * (tw_entries<N, SW>() + kR16TwEntries);
+  static constexpr size_t kBlockBytes = sizeof(float2) * (N + kR16TwEntries);
 
   __device__ EngP1024(char* lds, int wave, int lane_) : FusedOps<EngP1024, 8, 9>(lds, wave, lane_, N / 2) {}
   static __device__ void block_init(char* lds) {
     float2* t = reinterpret_cast<float2*>(lds);
-    init_twiddles<N, SW>(t);
+    init_twiddles<N>(t);
     for (int e = threadIdx.x; e < kR16TwEntries; e += blockDim.x) {
       const int Ls = e < 48 ? 16 : (e < 60 ? 4 : 64), o = e - (Ls == 16 ? 0 : (Ls == 4 ? 48 : 60));
       const int j = o / Ls, k = o % Ls, mult = j == 0 ? 1 : (j == 1 ? 4 : 8);
@@ -930,38 +876,27 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
     }
   }
 
-  // the four outputs of radix-4 butterfly i of a span-1 stage (out[4 i + q] in the swizzled layout, whose 4-element
-  // groups stay contiguous: lds_idx<SW>(4 i + q) = 4 i' + q) as two 16-byte stores at a 32-byte
+  // the four outputs of radix-4 butterfly i of a span-1 stage (out[4 i + q]) as two 16-byte stores at a 32-byte
   // lane stride; lanes with i & 4 store their second pair first so that every 8-lane store group tiles the 32 banks
   // (as EngF500's stage 1)
   static __device__ __forceinline__ void store4(float2* out, int i, float2 x0, float2 x1, float2 x2, float2 x3) {
     const bool sw = (i & 4) != 0;
     const int o = sw ? 2 : 0;
-    float4* d = reinterpret_cast<float4*>(out + lds_idx<SW>(4 * i));
+    float4* d = reinterpret_cast<float4*>(out + 4 * i);
     d[o >> 1] = sw ? make_float4(x2.x, x2.y, x3.x, x3.y) : make_float4(x0.x, x0.y, x1.x, x1.y);
     d[(2 - o) >> 1] = sw ? make_float4(x0.x, x0.y, x1.x, x1.y) : make_float4(x2.x, x2.y, x3.x, x3.y);
   }
 
   __device__ __forceinline__ void stage1(const float2 (&z)[8]) const {
-    if constexpr (R16) {
-      // radix-16 butterfly i = lane of x[i + 64 t], t < 16: the prefetched z[t] for t < 8, zero above; outputs
-      // out[16 i + q] at the padded index 17 i + q (16 lanes of a store group: 16 distinct banks)
-      float2 a[16];
+    // radix-16 butterfly i = lane of x[i + 64 t], t < 16: the prefetched z[t] for t < 8, zero above; outputs
+    // out[16 i + q] at the padded index 17 i + q (16 lanes of a store group: 16 distinct banks)
+    float2 a[16];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) a[t] = z[t];
-      dft16<true>(a);
-      float2* o = bufA + 17 * lane;
+    for (int t = 0; t < 8; ++t) a[t] = z[t];
+    dft16<true>(a);
+    float2* o = bufA + 17 * lane;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) o[q] = a[q];
-      return;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = lane + 64 * r;
-      const float2 a0 = z[r], a1 = z[r + 4];
-      // radix-4 DFT of (a0, a1, 0, 0)
-      store4(bufB, i, cadd(a0, a1), add_mi(a0, a1), csub(a0, a1), add_pi(a0, a1));
-    }
+    for (int q = 0; q < 16; ++q) o[q] = a[q];
   }
 
   // radix-16 Stockham stage (span Ls = 16, 4 or 64) of butterfly i = lane: inputs in[ia(i + 64 t)], twiddles
@@ -972,13 +907,8 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
     float2 a[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) a[t] = lds_ld(in, ia(i + 64 * t));
-#if DVH_P1024_R16TW
     const float2* st = tw + r16_tw(Ls);
     twiddle16(a, st[k], st[Ls + k], st[2 * Ls + k]);
-#else
-    constexpr int TWS = N / (16 * Ls);
-    twiddle16(a, tw[k * TWS], tw[4 * k * TWS], tw[8 * k * TWS]);
-#endif
     dft16<false>(a);
     const int base = (i - k) * 16 + k;
 #pragma unroll
@@ -987,9 +917,8 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
 
   // radix-4 butterfly k of the last stage (span 256): X[k + 256 q], q < 4
   __device__ __forceinline__ void last_bfly_from(const float2* src, int k, float2 (&x)[4]) const {
-    const int kb = lds_idx<SW>(k);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) x[t] = lds_ld(src, kb + 256 * t);
+    for (int t = 0; t < 4; ++t) x[t] = lds_ld(src, k + 256 * t);
     const float2 w1 = tw[k];
     float2 wt = w1;
 #pragma unroll
@@ -1009,18 +938,8 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
   template <class F>
   __device__ __forceinline__ void finish_with(F&& acc) const {
     wave_sync();
-    const float2* src;  // the span-256 stage's input
-    if constexpr (R16) {
-      stage16<16>(bufA, bufB, [](int n) { return n + (n >> 4); }, [](int n) { return n; });
-      src = bufB;
-    } else {
-      stockham_stage<N, 4, 4, SW>(bufB, bufA, tw, lane);
-      wave_sync();
-      stockham_stage<N, 16, 4, SW>(bufA, bufB, tw, lane);
-      wave_sync();
-      stockham_stage<N, 64, 4, SW>(bufB, bufA, tw, lane);
-      src = bufA;
-    }
+    stage16<16>(bufA, bufB, [](int n) { return n + (n >> 4); }, [](int n) { return n; });
+    const float2* src = bufB;  // the span-256 stage's input
     wave_sync();
     const int ln = opaque(lane);  // the stage's addresses formed per call, not held in registers between calls
     const bool l0 = ln == 0;
@@ -1070,20 +989,9 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
     bfly(l0 ? 128 : 192 - ln, sel(l0, A(2), A(6)), sel(l0, A(3), A(7)), sel(l0, B(3), B(5)), sel(l0, B(2), B(4)));
     bfly(l0 ? 192 : 256 - ln, sel(l0, A(6), A(2)), sel(l0, A(7), A(3)), sel(l0, B(5), B(1)), sel(l0, B(4), B(0)));
     wave_sync();
-    if constexpr (R16) {
-      stage16<4>(bufB, bufA, [](int n) { return n; }, [](int n) { return n + 4 * (n >> 6); });
-      wave_sync();
-      stage16<64>(bufA, bufB, [](int n) { return n + 4 * (n >> 6); }, [](int n) { return n; });
-      wave_sync();
-      return bufB;
-    }
-    stockham_stage<N, 4, 4, SW>(bufB, bufA, tw, lane);
+    stage16<4>(bufB, bufA, [](int n) { return n; }, [](int n) { return n + 4 * (n >> 6); });
     wave_sync();
-    stockham_stage<N, 16, 4, SW>(bufA, bufB, tw, lane);
-    wave_sync();
-    stockham_stage<N, 64, 4, SW>(bufB, bufA, tw, lane);
-    wave_sync();
-    stockham_stage<N, 256, 4, SW>(bufA, bufB, tw, lane);
+    stage16<64>(bufA, bufB, [](int n) { return n + 4 * (n >> 6); }, [](int n) { return n; });
     wave_sync();
     return bufB;
   }
@@ -1098,9 +1006,9 @@ struct EngP1024 : FusedOps<EngP1024, 8, 9> {
 
   // (N * sum_s c_f[k], N * sum_s c_o[k]): the linear correlation folded to the circular one of period w
   __device__ float2 c(const float2* Y, int k, int w_) const {
-    float2 v = Y[lds_idx<SW>(k)];
+    float2 v = Y[k];
     if (k > 0) {
-      const float2 u = Y[lds_idx<SW>(N - w_ + k)];
+      const float2 u = Y[N - w_ + k];
       v.x += u.x;
       v.y += u.y;
     }

@@ -213,7 +213,9 @@ int dvh_sosfiltfilt(void* x, int32_t dtype, int64_t n_rows, int64_t row_stride, 
  * plan NULL: the recursion, as dvh_sosfiltfilt).  Its rounding grows with the largest pole radius r (host sos: dvh_sos_pole_radius):
  * 1e-13 relative at r = 0.9956, 5e-10 at r = 0.99973, so plan it only for r <= DVH_SOS_MFMA_MAX_POLE.
  * bandpass_data (modules/utils.py:179-189) called once per record of the same shape designs the same filter every
- * time; the drop-in caches the plan per (design, n_t). */
+ * time; the drop-in caches the plan per (design, n_t).  A plan is valid only for the (n_t, padlen) it was formed for:
+ * it records its group sizes, and a call whose scans need another group transition gets NaN in the output there
+ * (records short enough to need no carried groups never read the transition and filter correctly). */
 #define DVH_SOS_MFMA_MAX_POLE 0.999
 double dvh_sos_pole_radius(const double* sos_host, int32_t n_sec);
 int64_t dvh_sosfiltfilt_plan_bytes(int32_t n_sec);

@@ -602,3 +602,15 @@ def test_sosfiltfilt_rejects_misaligned_workspace():
         args = (fake, 0, 4, 3000, 3000, fake, 10, 63, fake) + extra + (ctypes.c_void_p(0x1008), None)
         assert getattr(lib, name)(*args) == -2
         assert b"16-byte aligned" in lib.dvh_last_error()
+
+
+def test_save_images_raises_before_imaging():
+    """save_images (apis/imaging_classes.py:110-117) points at the reference's plotting with no device work, also on
+    the sharded flavour-B path whose per-pass images are never formed (images is None)."""
+    from das_diff_veh_amd.apis.imaging_classes import DispersionImagesFromWindows, VirtualShotGathersFromWindows
+    d = DispersionImagesFromWindows([])
+    d.images = None
+    with pytest.raises(NotImplementedError, match="were not formed"):
+        d.save_images("/nonexistent")
+    with pytest.raises(NotImplementedError, match="plot_xcorr"):
+        VirtualShotGathersFromWindows([]).save_images("/nonexistent")

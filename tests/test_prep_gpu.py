@@ -109,20 +109,72 @@ def test_matrix_form_only_for_poles_clear_of_the_unit_circle(device):
         assert (plan is not None) == planned
 
 
-@pytest.mark.parametrize("n_t", [130, 700, 4000, 15500, 16600])
-def test_matrix_form_record_lengths(device, n_t):
+@pytest.mark.parametrize("n_rows,n_t", [(48, 130), (48, 700), (48, 4000), (48, 15500), (48, 16600), (45, 130),
+                                          (47, 700)])
+def test_matrix_form_record_lengths(device, n_rows, n_t):
     """The matrix-pipe form across the scans it dispatches to: records of 4 blocks (one group holds every block),
     mid-size records (groups of 1-3 blocks, some of the 16 groups empty), 15 500 samples (16 groups of 16 blocks, the
-    last partial: the matrix-pipe scan's limit) and 16 600 (past it: the staged scan), float64 rows against
-    scipy.signal.sosfiltfilt as bandpass_data calls it (1e-10)."""
+    last partial: the matrix-pipe scan's limit) and 16 600 (past it: the staged scan); 45 x 130 and 47 x 700 leave a
+    partial last tile of 16 columns spanning 3+ rows, whose padding columns (rows >= n_rows) must read nothing.
+    float64 rows against scipy.signal.sosfiltfilt as bandpass_data calls it (1e-10)."""
     import torch
 
     from das_diff_veh_amd.preprocess import bandpass_inplace
     from oracle import preprocess as oprep
     rng = np.random.default_rng(n_t)
     dt = 0.004
-    host = rng.standard_normal((48, n_t)) + np.sin(2 * np.pi * 7.0 * np.arange(n_t) * dt)[None, :]
+    host = rng.standard_normal((n_rows, n_t)) + np.sin(2 * np.pi * 7.0 * np.arange(n_t) * dt)[None, :]
     dev = torch.from_numpy(host.copy()).to(device)
     bandpass_inplace(dev, dt, 1.2, 30)
     ref = oprep.bandpass_data_scipy(host, dt, 1.2, 30)
     assert np.abs(dev.cpu().numpy() - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+def _planned_run(device, sos, host, plan_n_t):
+    """dvh_sosfiltfilt_plan for a record of plan_n_t samples, then dvh_sosfiltfilt_planned on host's rows."""
+    import scipy.signal
+    import torch
+
+    from das_diff_veh_amd import _lib
+    from das_diff_veh_amd.preprocess import _padlen
+    n_rows, n_t = host.shape
+    padlen = _padlen(sos)
+    sos_t = torch.from_numpy(np.ascontiguousarray(sos, dtype=np.float64)).to(device)
+    zi_t = torch.from_numpy(np.ascontiguousarray(scipy.signal.sosfilt_zi(sos), dtype=np.float64)).to(device)
+    dev = torch.from_numpy(host.copy()).to(device)
+    nbytes = int(_lib.load().dvh_sosfiltfilt_workspace(n_rows, n_t, len(sos), padlen))
+    work = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+    plan = torch.empty(int(_lib.load().dvh_sosfiltfilt_plan_bytes(len(sos))) // 8, dtype=torch.float64, device=device)
+    _lib.call("dvh_sosfiltfilt_plan", _lib.ptr(sos_t), len(sos), _lib.ptr(zi_t), plan_n_t, padlen, _lib.ptr(plan),
+              _lib.stream_of(device))
+    _lib.call("dvh_sosfiltfilt_planned", _lib.ptr(dev), 1, n_rows, dev.stride(0), n_t, _lib.ptr(sos_t), len(sos),
+              padlen, _lib.ptr(zi_t), _lib.ptr(plan), _lib.ptr(work), _lib.stream_of(device))
+    return dev.cpu().numpy()
+
+
+def test_matrix_form_low_order_lds_resident_scan(device):
+    """A 4-section design (butter(4, band)) on a 20 000-sample record: 314 blocks, past the matrix-pipe scan's 258 and
+    inside the LDS-resident VALU scan's range at 8 state components (sosm_scanr_kernel, which the drop-in's 10-section
+    design never reaches), against scipy.signal.sosfiltfilt at 1e-10."""
+    import scipy.signal
+    dt = 0.004
+    sos = scipy.signal.butter(4, [1.2 * 2 * dt, 30 * 2 * dt], "bandpass", output="sos")
+    assert len(sos) == 4
+    rng = np.random.default_rng(4)
+    n_t = 20000
+    host = rng.standard_normal((40, n_t)) + np.sin(2 * np.pi * 7.0 * np.arange(n_t) * dt)[None, :]
+    got = _planned_run(device, sos, host, n_t)
+    ref = scipy.signal.sosfiltfilt(sos, host, axis=1)
+    assert np.abs(got - ref).max() <= 1e-10 * np.abs(ref).max()
+
+
+def test_plan_for_another_record_length_poisons_the_output(device):
+    """A plan carries the group size its group transitions were formed for: planned for 4 000 samples and run on
+    15 000 (another group size, carried groups in use), the output holds NaN instead of a silently wrong filter."""
+    from das_diff_veh_amd.preprocess import butter_bandpass_sos
+    sos = butter_bandpass_sos(0.004, 1.2, 30)
+    host = np.random.default_rng(5).standard_normal((8, 15000))
+    got = _planned_run(device, sos, host, 4000)
+    assert np.isnan(got).any()
+    ok = _planned_run(device, sos, host, 15000)
+    assert np.isfinite(ok).all()

@@ -46,8 +46,8 @@ def test_save_disp_imgs_subset_stack_and_image(device, tmp_path, seed, min_win, 
 
 
 def test_save_images_points_at_plotting(device, tmp_path):
-    """ImagesFromWindows.save_images (apis/imaging_classes.py:110-117) exists on the drop-in classes and reaches the
-    images' plot_image, which raises with a pointer to the reference's plotting."""
+    """ImagesFromWindows.save_images (apis/imaging_classes.py:110-117) exists on the drop-in classes and raises with a
+    pointer to the reference's plotting, without materialising the per-pass gathers first."""
     from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
     from das_diff_veh_amd.apis.imaging_classes import VirtualShotGathersFromWindows
     g = gio.load("vsg_w500")
@@ -55,3 +55,4 @@ def test_save_images_points_at_plotting(device, tmp_path):
     images.get_images(include_other_side=True, pivot=700, start_x=500, end_x=900, wlen=2)
     with pytest.raises(NotImplementedError, match="plot"):
         images.save_images(str(tmp_path))
+    assert not images.images._done  # the lazily computed per-pass gathers were not formed
