@@ -390,9 +390,50 @@ def gen_tli(ref):
                 qs_first=obj.qs_selector.windows[0].data)
 
 
+def gen_workflow(ref):
+    """The xcorr flavour of the daily workflow, ImagingWorkflowOneDirectory.imaging (apis/imaging_workflow.py:33-80)
+    with method='xcorr' over two files: per file TimeLapseImaging's preprocessing (:50-71, method 'xcorr': no trace
+    norm), SurfaceWaveSelector (:166-196), get_images (:198-201: VirtualShotGathersFromWindows, norm=False, no mute),
+    then ``avg_image += imagingObj.images.avg_image`` from ``avg_image = 0`` (:39, :67: a sum of per-file means), and
+    at the end compute_disp_image() with its defaults and save_avg_disp_to_npz (:199-201, timeLapseImaging.py:205).
+    Each file's TimeLapseImaging is a plain object holding the tracking results (the tracker is outside the hot
+    path), as in gen_tli."""
+    import tempfile
+
+    import apis.timeLapseImaging as tli
+    from tests.golden_io import workflow_files
+    T = tli.TimeLapseImaging
+    out = {}
+    avg_image = 0
+    for k, c in enumerate(workflow_files()):
+        obj = types.SimpleNamespace(method="xcorr", data=c["rec"].copy(), dt=c["t_axis"][1] - c["t_axis"][0],
+                                    t_axis=c["t_axis"], x_axis=c["x_axis"],
+                                    distances_along_fiber=(c["x_axis"] - 400) * 8.16,
+                                    surface_wave_preprecessing_dict=None, start_x=c["start_x_tracking"],
+                                    veh_states=c["veh_states"], dist_along_fiber_tracking=c["dist_trk"],
+                                    t_axis_tracking=c["t_trk"])
+        T._preprocessing_for_surface_waves(obj)
+        T.select_surface_wave_windows(obj, c["x0"], **c["select_kw"])
+        T.get_images(obj, **c["imaging_kw"])
+        out[f"n_windows_{k}"] = np.array(len(obj.sw_selector.windows))
+        out[f"w_{k}"] = np.array([im.XCF_out.shape[-1] for im in obj.images.images])
+        out[f"file_avg_{k}"] = obj.images.avg_image.XCF_out
+        avg_image += obj.images.avg_image
+    avg_image.compute_disp_image()
+    out.update(day_xcf=avg_image.XCF_out, day_x_axis=avg_image.x_axis, day_t_axis=avg_image.t_axis,
+               day_fv=avg_image.disp.fv_map)
+    with tempfile.TemporaryDirectory() as d:
+        T.save_avg_disp_to_npz(types.SimpleNamespace(images=types.SimpleNamespace(avg_image=avg_image)),
+                               fname="day.npz", fdir=d)
+        f = np.load(os.path.join(d, "day.npz"), allow_pickle=False)
+        out["npz_keys"] = np.array(sorted(f.files))
+        assert np.array_equal(f["XCF_out"], avg_image.XCF_out)
+    return out
+
+
 GENERATORS = {"vsg_w500": gen_vsg, "vsg_w499": gen_vsg_w499, "vsg_edge": gen_vsg_edge, "disp": gen_disp,
               "bandpass": gen_bandpass, "ridge": gen_ridge, "fk": gen_fk, "prep": gen_prep, "select": gen_select,
-              "tli": gen_tli}
+              "tli": gen_tli, "workflow": gen_workflow}
 
 
 def main(names=None):

@@ -83,3 +83,37 @@ def select_cases():
                                                               temporal_spacing=0.5)),
         "spacing": dict(base, veh_states=states(mixed), kw=dict(wlen_sw=1, length_sw=150, temporal_spacing=1.05)),
     }
+
+
+def workflow_files():
+    """Two synthetic "files" of one day for ImagingWorkflowOneDirectory.imaging (apis/imaging_workflow.py:33-80)
+    with method='xcorr': continuous records of 48 ch x 9 000 samples on a time axis starting at t = 4 s (so that no
+    window's t_axis[1] - t_axis[0] is exactly 0.004, where the reference raises; the windows' steps then round to
+    w = 500 or 499 by their start, and the class means mix both, as on real records), tracked vehicles at varied
+    speeds (seconds per 1 m tracking column), x0 = 620; wlen_sw = 12 s windows (3 000 samples: room for the pivot's
+    4 s correlation window on both sides).  File A accepts 2 of 3 passes (the last window runs past the record),
+    file B 2 of 3 (the same)."""
+    from das_diff_veh_amd.synth import DT_W500
+    n_ch, n_t, dt = 48, 9000, 0.004
+    dist_trk = 380.0 + np.arange(400.0)  # the 1 m tracking grid (resample_poly 204 / 25 of the 8.16 m channels)
+    t_trk = DT_W500 + np.arange(0, n_t * dt, 0.012)
+    n_x = 100
+
+    def states(tc, spc):
+        vs = np.full((len(tc), n_x), np.nan)
+        for k, (t, s) in enumerate(zip(tc, spc)):
+            times = t + (np.arange(n_x) - 25) * s
+            ok = (times >= 0) & (times < t_trk[-1])
+            vs[k, ok] = np.round(times[ok] / 0.012)
+            vs[k, :2] = np.nan
+        return vs
+
+    files = []
+    for seed, tc, spc in ((710, [7.0, 19.5, 32.0], [0.05, 0.04, 0.06]), (711, [6.2, 18.4, 30.6], [0.055, 0.045, 0.05])):
+        rng = np.random.default_rng(seed)
+        rec = np.round(rng.standard_normal((n_ch, n_t)) * 2 ** 8) / 2 ** 8  # exact in float32
+        files.append(dict(rec=rec, x_axis=449.0 + np.arange(n_ch), t_axis=DT_W500 + np.arange(n_t) * dt, x0=620,
+                          start_x_tracking=595, veh_states=states(tc, spc), dist_trk=dist_trk, t_trk=t_trk,
+                          select_kw=dict(wlen_sw=12, length_sw=300, spatial_ratio=0.75),
+                          imaging_kw=dict(pivot=620, start_x=500, end_x=680, wlen=2, include_other_side=True)))
+    return files

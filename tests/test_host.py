@@ -614,3 +614,14 @@ def test_save_images_raises_before_imaging():
         d.save_images("/nonexistent")
     with pytest.raises(NotImplementedError, match="plot_xcorr"):
         VirtualShotGathersFromWindows([]).save_images("/nonexistent")
+
+
+def test_workflow_requires_imaging_kwargs():
+    """ImagingWorkflowOneDirectory.imaging (apis/imaging_workflow.py:33-80) with the reference's default
+    imaging_kwargs=None fails as the reference's get_images(**None) does, before any record is read."""
+    from das_diff_veh_amd.apis.imaging_workflow import ImagingWorkflowOneDirectory
+    wf = ImagingWorkflowOneDirectory(iter(()), [], method="xcorr")
+    with pytest.raises(TypeError):
+        wf.imaging(595, 700, 620)
+    with pytest.raises(NotImplementedError):
+        wf.plot_avg_images()
