@@ -63,12 +63,14 @@ def build(verbose=False, jobs=None, out=None, defines=(), flags=()):
         objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
         return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    tmp = LIB + ".tmp"  # linked aside and renamed: a reader never sees a partly written library
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
     return LIB
 
 

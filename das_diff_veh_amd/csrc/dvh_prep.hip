@@ -369,8 +369,19 @@ __global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* _
 // a float64 model of this scheme matches scipy.signal.sosfiltfilt to 1e-13); tests/test_prep_gpu.py holds them to
 // scipy at 1e-10 (float64) / 2e-6 (float32).
 constexpr int kSmL = 64;     // samples per block: four 16-row MFMA tiles
-constexpr int kSmLd = 66;    // LDS image row stride (doubles): B-operand reads (column li, sample 4 kk + q) of 32
-                             // lanes hit 32 distinct banks (2 li + q)
+#ifndef DVH_SOSM_LD
+#define DVH_SOSM_LD 65
+#endif
+#ifndef DVH_SOSM_GA
+#define DVH_SOSM_GA 33
+#endif
+#ifndef DVH_SOSM_OCC
+#define DVH_SOSM_OCC 3
+#endif
+constexpr int kSmLd = DVH_SOSM_LD;  // LDS image row stride (doubles), odd: the B-operand reads (column li, sample
+                                    // 4 kk + q), which the compiler pairs into ds_read2_b64 (16-lane groups, 32 banks),
+                                    // and the accumulator stores (ds_write_b64, 16-lane groups) of the 16 columns land
+                                    // on 16 distinct bank pairs (at 66 they fell on 8: 2-way conflicts)
 constexpr int kSmRows = 32;  // state rows of the MFMA tiles (2 NS <= 32)
 typedef double doublex4_t __attribute__((ext_vector_type(4)));
 
@@ -498,7 +509,7 @@ __device__ __forceinline__ double sosm_ext(const T* __restrict__ x, const SosGeo
 //     Toeplitz factors T[i][j] = h[i - j] = hq[q][64 + i - j] and U[i][j] = h[j - i] = hr[q][64 + i - j]
 //   hm[i][m] = Hm[i][m], stride 21;  ga[j][m] = g[L - 1 - j][m], stride 48;  gb[m][i] = g[i][m], stride 66
 //   (rows m >= 2 NS zero)
-constexpr int kHq = 145, kHmLd = 21, kGaLd = 48, kGbLd = 66;
+constexpr int kHq = 145, kHmLd = 21, kGaLd = DVH_SOSM_GA, kGbLd = DVH_SOSM_LD;
 template <int NS>
 __device__ __forceinline__ void sosm_tables(const double* __restrict__ mats, double* hq, double* hr, double* hm, double* ga,
                                             double* gb) {
@@ -678,7 +689,7 @@ __device__ __forceinline__ void sosm_states_out(double* img, int lane, const dou
 
 // Forward phase A: E_f[c] = G u_block for k < nb - 1 (block 0: + M zi u_0, its true end state).
 template <typename T, int NS>
-__global__ __launch_bounds__(256) void sosm_fa_kernel(const T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
+__global__ __launch_bounds__(256, DVH_SOSM_OCC) void sosm_fa_kernel(const T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
                                                       double* __restrict__ Sf) {
   using O = SosmMats<NS>;
   constexpr int NST = 2 * NS;
@@ -930,7 +941,7 @@ __global__ __launch_bounds__(64) void sosm_bf_kernel(T* __restrict__ x, SosGeom 
 // Backward phase C for backward blocks k' >= 1 (forward blocks k = nb - 1 - k' < nb - 1, columns (r, k) of an
 // [n_rows][nb - 1] grid): v = U y + Hrev s with s the true backward state before the block, trimmed into the row.
 template <typename T, int NS>
-__global__ __launch_bounds__(256) void sosm_bc_kernel(T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
+__global__ __launch_bounds__(256, DVH_SOSM_OCC) void sosm_bc_kernel(T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
                                                       const double* __restrict__ y, const double* __restrict__ Sb) {
   constexpr int NST = 2 * NS, KS = (NST + 3) / 4;
   __shared__ double hr[4 * kHq], hm[kSmL * kHmLd], imgs[4][16 * kSmLd];

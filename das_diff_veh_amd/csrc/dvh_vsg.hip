@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -125,6 +126,31 @@ __device__ __forceinline__ int xcd_block() {
   const int q = G / 8, r = G % 8, x = b % 8, k = b / 8;
   return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
 }
+
+// The row tasks [0, n) of a stack launch as one wave takes them: a static stride (t0, t0 + stride, ...), pulled from
+// one global counter, or pulled from eight per-XCD counters -- XCD x first drains its own contiguous eighth of the
+// tasks, then the other XCDs' leftovers -- so that the row tasks of a chunk, which read the chunk's windows and pivot
+// tables, run in one XCD's L2 while the waves stay balanced.
+struct TaskSource {
+  uint32_t* q = nullptr;  // nullptr: static stride; else one counter, or 8 per-XCD counters (xcd)
+  bool xcd = false;
+  int64_t n = 0, stride = 1;
+  int cur = 0;  // per-XCD: queues tried so far (wave-uniform)
+  __device__ int64_t pull(int lane) {
+    if (!xcd) return pull_unit(q, lane);
+    const int x = blockIdx.x & 7;  // workgroups are dealt round robin over the 8 XCDs
+    while (cur < 8) {
+      const int y = (x + cur) & 7;
+      const int64_t b = n * y / 8, e = n * (y + 1) / 8;
+      const int64_t t = b + pull_unit(q + y, lane);
+      if (t < e) return t;
+      ++cur;
+    }
+    return n;
+  }
+  __device__ int64_t first(int64_t t0, int lane) { return q ? pull(lane) : t0; }
+  __device__ int64_t next(int64_t t, int lane) { return q ? pull(lane) : t + stride; }
+};
 
 template <class E>
 __device__ __forceinline__ E make_engine(char* lds) {
@@ -342,8 +368,7 @@ template <class E>
 __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
-                                             float* __restrict__ stack, int64_t t0, int64_t stride,
-                                             uint32_t* tq = nullptr) {
+                                             float* __restrict__ stack, int64_t t0, TaskSource src) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -352,40 +377,25 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
   const bool norm = (A.flags & kFlagNorm) != 0;
   const int h = N / 2;
   const int64_t n_task = (int64_t)n_chunk * A.R;
-  // tasks t0, t0 + stride, ... (static), or pulled from the counter tq; the next index fetched at the top of
-  // the task so that `continue` moves on
+  // tasks from src (static stride or pulled); the next index fetched at the top of the task so that `continue`
+  // moves on
   const int lane_t = threadIdx.x & 63;
-  int64_t tn = tq ? pull_unit(tq, lane_t) : t0;
+  src.n = n_task;
+  int64_t tn = src.first(t0, lane_t);
   for (int64_t t = tn; t < n_task; t = tn) {
-    tn = tq ? (int64_t)pull_unit(tq, lane_t) : t + stride;
+    tn = src.next(t, lane_t);
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
-    int np = -1, ni = 0;
-    if (E::kNextTask && t + stride < n_task) {
-      const int c2 = uni((int)((t + stride) / A.R));
-      ni = uni((int)((t + stride) % A.R));
-      const int b2 = sld(chunk_tab + 3 * c2);
-      if (b2 < sld(chunk_tab + 3 * c2 + 1)) np = sld(order + b2);
-    }
     float* o = stack + ((int64_t)slot * A.R + i) * A.w;
     float2 Gh[NH];
 #pragma unroll
     for (int m = 0; m < NH; ++m) Gh[m] = make_float2(0.f, 0.f);
-    RowTask task = (E::kNextTask && b < e) ? make_task(A, sld(order + b), i) : RowTask{};
     const bool direct = !norm && engine_direct<E, true>(eng, A, scales, order, weight, b, e, i, Gh);
     for (int q = direct ? e : b; q < e; ++q) {
       const int p = sld(order + q);
-      RowTask tn = task;
-      bool has_next = false;
-      if (E::kNextTask) {  // engines that prefetch the next task's first sub-window get it
-        has_next = (q + 1 < e) || np >= 0;
-        if (q + 1 < e) tn = make_task(A, sld(order + q + 1), i);
-        else if (np >= 0) tn = make_task(A, np, ni);
-      } else {
-        task = make_task(A, p, i);
-      }
+      const RowTask task = make_task(A, p, i);
       float2 Cf[NH], Co[NH];
-      engine_spectra(eng, A, task, tn, has_next, Cf, Co);
+      engine_spectra(eng, A, task, task, false, Cf, Co);
       const float sf = sld(scales + 2 * p), so = sld(scales + 2 * p + 1), wp = sld(weight + p);
       // per-pass bin / twiddle-index math recomputed here (hoisted, it only spills)
       const int lane = opaque(lane_);
@@ -401,6 +411,9 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
       }
       const bool bad = __ballot(isnan(af + ao)) != 0;
       const bool nzo = other && (__ballot(ao != 0.f) != 0);
+      if constexpr (Fused<E>::v) {  // covered-span scan: a non-finite sample among this pass's loaded slices
+        if (eng.vflag && __ballot(!isfinite(af + ao)) != 0 && lane_ == 0) atomicMax(eng.vflag + p, kInfBits);
+      }
       float ff, fo;
       if (norm) {  // ||c||^2 = sum_m |C[m]|^2 / N (Parseval over all N bins: interior bins count twice)
         float s2f = 0.f, s2o = 0.f;
@@ -461,7 +474,6 @@ __device__ __forceinline__ void stackf_tasks(E& eng, const VsgArgs& A, const flo
           }
         }
       }
-      task = tn;
     }
     float2 Z[NH];
 #pragma unroll
@@ -492,8 +504,7 @@ template <class E>
 __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                              const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                              int32_t n_chunk, const float* __restrict__ weight,
-                                             float* __restrict__ stack, int64_t t0, int64_t stride,
-                                             uint32_t* tq = nullptr) {
+                                             float* __restrict__ stack, int64_t t0, TaskSource src) {
   const int lane_ = threadIdx.x & 63;
   constexpr int NJ = E::NJ;
   constexpr int NH = E::NH;
@@ -502,12 +513,13 @@ __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const flo
   const bool norm = (A.flags & kFlagNorm) != 0;
   const int w = A.w, h = w / 2;
   const int64_t n_task = (int64_t)n_chunk * A.R;
-  // tasks t0, t0 + stride, ... (static), or pulled from the counter tq; the next index fetched at the top of
-  // the task so that `continue` moves on
+  // tasks from src (static stride or pulled); the next index fetched at the top of the task so that `continue`
+  // moves on
   const int lane_t = threadIdx.x & 63;
-  int64_t tn = tq ? pull_unit(tq, lane_t) : t0;
+  src.n = n_task;
+  int64_t tn = src.first(t0, lane_t);
   for (int64_t t = tn; t < n_task; t = tn) {
-    tn = tq ? (int64_t)pull_unit(tq, lane_t) : t + stride;
+    tn = src.next(t, lane_t);
     const int c = uni((int)(t / A.R)), i = uni((int)(t % A.R));
     const int b = sld(chunk_tab + 3 * c), e = sld(chunk_tab + 3 * c + 1), slot = sld(chunk_tab + 3 * c + 2);
     float* o = stack + ((int64_t)slot * A.R + i) * A.w;
@@ -608,8 +620,9 @@ __global__ __launch_bounds__(64 * E::kWaves, OccP<E>::v) void vsg_stackp_kernel(
   E eng = make_engine<E>(lds);
   bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6;
-  stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave,
-                  (int64_t)gridDim.x * E::kWaves);
+  TaskSource src;
+  src.stride = (int64_t)gridDim.x * E::kWaves;
+  stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave, src);
 }
 
 template <class E>
@@ -621,8 +634,9 @@ __global__ __launch_bounds__(64 * E::kWaves, OccF<E>::v) void vsg_stackf_kernel(
   E eng = make_engine<E>(lds);
   bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6;
-  stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave,
-                  (int64_t)gridDim.x * E::kWaves);
+  TaskSource src;
+  src.stride = (int64_t)gridDim.x * E::kWaves;
+  stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * E::kWaves + wave, src);
 }
 
 // The pivot-slice spectra table of every pass (FusedOps::spectra_tab) for engine E: one wave per pass forms the
@@ -782,11 +796,125 @@ struct ScanArgs {
   int32_t n_ch, n_t;   // rows and samples of one window
 };
 
-// Pull scan units (window, kScanRows channel rows) until none is left; atomicMax into vflag[window].
+// ---- covered-span scan: the scan leaves out, per gather row, the float4s inside the row's correlated slices
+// [a, a + (nwin - 1) hop + w) (both sides), which the correlation waves load and validate themselves (non-finite
+// samples reach their spectra, or are checked where a sub-window is not transformed: FusedOps::check_untransformed).
+// A row's remaining float4s are at most three spans; the wave streams them as one virtual index range, each lane's
+// load address mapped past the skipped ranges (two compares), with kScanDepth loads in flight across row boundaries.
+// Windows whose flag ends at 0 (nothing non-zero in the scanned part) or kSuspect are rescanned whole afterwards
+// (window_fixup_kernel), so all-zero windows and non-finite spectra without a pass stay exact.
+struct SpanRow {
+  uint32_t base;  // byte offset of the row in the window (windows < 4 GiB)
+  int U;         // float4s to scan
+  int t0, d0;    // virtual index of the first skipped range, its length (float4)
+  int s1, d1;    // start (real float4 index) and length of the second
+};
+// float4 range wholly inside side (a, L)'s correlated slices (empty when hop > w leaves gaps)
+__device__ __forceinline__ void covered4(int a, int L, int w, int hop, int& b, int& e) {
+  const int nw = n_subwin(L, w, hop);
+  b = e = 0;
+  if (nw <= 0 || hop > w) return;
+  b = (a + 3) >> 2;
+  e = (a + (nw - 1) * hop + w) >> 2;
+  if (e < b) b = e = 0;
+}
+__device__ __forceinline__ SpanRow span_row(const VsgArgs& A, int p, int row0, int c, int n4) {
+  SpanRow r;
+  r.base = (uint32_t)((int64_t)c * A.ch_stride * 4);
+  int b0 = 0, e0 = 0, b1 = 0, e1 = 0;
+  const int i = c - row0;
+  if (i >= 0 && i < A.R) {
+    const int32_t* seg = A.seg_tab + ((int64_t)p * A.R + i) * 4;
+    covered4(sld(seg), sld(seg + 1), A.w, A.hop, b0, e0);
+    if (A.flags & kFlagOtherSide) covered4(sld(seg + 2), sld(seg + 3), A.w, A.hop, b1, e1);
+  }
+  if (e0 <= b0) b0 = e0 = n4;  // empty ranges sit past the row
+  if (e1 <= b1) b1 = e1 = n4;
+  if (b1 < b0) {  // ordered
+    int t = b0; b0 = b1; b1 = t;
+    t = e0; e0 = e1; e1 = t;
+  }
+  if (b1 < e0) {  // overlapping ranges merge
+    e0 = max(e0, e1);
+    b1 = e1 = n4;
+  }
+  e0 = min(e0, n4);
+  e1 = min(e1, n4);
+  r.t0 = b0;
+  r.d0 = e0 - b0;
+  r.s1 = b1;
+  r.d1 = e1 - b1;
+  r.U = n4 - r.d0 - r.d1;
+  if (r.U == 0) r.U = 1;  // a wholly covered row reads one float4 again: no row is empty (one row switch per load)
+  return r;
+}
+// rows [c0, c1) of pass p's window (n_t % 4 == 0, 16-byte aligned rows): max |x| bit pattern over the wave
+__device__ __forceinline__ uint32_t scan_rows_span(const VsgArgs& A, const ScanArgs& S, int p, int c0, int c1, int lane) {
+  const float* base = A.win + (int64_t)p * A.pass_stride;
+  const int64_t wbytes = ((int64_t)(S.n_ch - 1) * A.ch_stride + S.n_t) * 4;  // < 0xfffffff0 (host)
+  const __amdgpu_buffer_rsrc_t rs = scan_rsrc(base, (uint32_t)wbytes);
+  const int row0 = sld(A.pass_tab + 2 * p), n4 = S.n_t >> 2;
+  constexpr uint32_t kOut = 0xfffffff0u;  // past the descriptor's range: the load returns 0
+  int c = c0, k = 0;
+  SpanRow cur = span_row(A, p, row0, c, n4);
+  auto issue = [&]() -> uint32_t {
+    if (c < c1 && k * 64 >= cur.U) {  // next row (the loads in flight cover its table reads)
+      ++c;
+      k = 0;
+      if (c < c1) cur = span_row(A, p, row0, c, n4);
+    }
+    if (c >= c1) return kOut;
+    const int v = k * 64 + lane;
+    ++k;
+    int o = v + (v >= cur.t0 ? cur.d0 : 0);
+    o += o >= cur.s1 ? cur.d1 : 0;
+    return v < cur.U ? cur.base + (uint32_t)o * 16u : kOut;
+  };
+  constexpr int D = 8;  // loads per lane in flight (16 spills: the kernel's registers are sized for the correlation)
+  uint32_t m = 0;
+  u32x4 r[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, issue(), 0, kScanAux);
+  while (c < c1) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const u32x4 v = r[d] & 0x7fffffffu;
+      m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+      r[d] = __builtin_amdgcn_raw_buffer_load_b128(rs, issue(), 0, kScanAux);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const u32x4 v = r[d] & 0x7fffffffu;
+    m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+  }
+  return wave_max_u32(m);
+}
+
+// Windows the covered-span scan could not decide -- flag 0 (the scanned part all zero: the slices may not be) or
+// kSuspect -- are rescanned whole: one block per window, nothing to do for the usual flag.
+__global__ __launch_bounds__(256) void window_fixup_kernel(VsgArgs A, ScanArgs S, uint32_t* __restrict__ vflag) {
+  const int s = blockIdx.x;
+  const uint32_t f0 = vflag[s];
+  if (f0 != 0 && !(f0 & kSuspect)) return;
+  __shared__ uint32_t part[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float* base = A.win + (int64_t)s * A.pass_stride;
+  uint32_t m = 0;
+  for (int c = wave; c < S.n_ch; c += 4)
+    for (int t = lane; t < S.n_t; t += 64) m = max(m, absbits(base[(int64_t)c * A.ch_stride + t]));
+  m = wave_max_u32(m);
+  if (lane == 0) part[wave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) vflag[s] = max(max(part[0], part[1]), max(part[2], part[3]));
+}
+
+// Pull scan units (window, kScanRows channel rows) until none is left; atomicMax into vflag[window].  span: the
+// covered-span scan (default windows of a launch whose chunks list every pass).
 template <int D = kScanDepth>
 __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, uint32_t* __restrict__ vflag,
                                            uint32_t* __restrict__ counter, int lane,
-                                           const int32_t* __restrict__ sorder = nullptr) {
+                                           const int32_t* __restrict__ sorder = nullptr, bool span = false) {
   const int upp = (S.n_ch + kScanRows - 1) / kScanRows;  // units per window
   const int n_units = S.n_win * upp;
   const bool vec = (S.n_t % 4 == 0) && (A.ch_stride % 4 == 0) && (A.pass_stride % 4 == 0) &&
@@ -797,7 +925,8 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
     const int q = u / upp, c0 = (u - q * upp) * kScanRows;
     const int s = (sorder && !S.tab) ? sld(sorder + q) : q;
     const float* base = S.tab ? A.win + (int64_t)sld(S.tab + s) * A.ch_stride : A.win + (int64_t)s * A.pass_stride;
-    const uint32_t m = scan_rows<D>(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
+    const uint32_t m = span ? scan_rows_span(A, S, s, c0, min(c0 + kScanRows, S.n_ch), lane)
+                            : scan_rows<D>(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
     if (lane == 0) atomicMax(vflag + s, m);
     u = un;
   }
@@ -813,9 +942,9 @@ template <class E, bool EXACT>
 __device__ __forceinline__ void stack_tasks(E& eng, const VsgArgs& A, const float* __restrict__ scales,
                                             const int32_t* __restrict__ order, const int32_t* __restrict__ chunk_tab,
                                             int32_t n_chunk, const float* __restrict__ weight, float* __restrict__ stack,
-                                            int64_t t0, int64_t stride, uint32_t* tq) {
-  if constexpr (EXACT) stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq);
-  else stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, stride, tq);
+                                            int64_t t0, TaskSource src) {
+  if constexpr (EXACT) stackf_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, src);
+  else stackp_tasks<E>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, t0, src);
 }
 
 // Persistent validated stack launch: blocks of kFft correlation waves + kScan scan waves (EngF500: two per CU;
@@ -825,24 +954,35 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
     const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
     float* __restrict__ stack, ScanArgs S, uint32_t* __restrict__ vflag, uint32_t* __restrict__ counter,
-    const float2* __restrict__ ptab) {
+    const float2* __restrict__ ptab, uint32_t* __restrict__ xq, int32_t span_req) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
   bind_engine(eng, A, ptab);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // the padded engines' correlation waves pull row tasks from a counter (w = 499: fused launch 4.80 -> 3.99 ms, their
-  // task costs vary with the pivot-slice table's coverage); the exact ones keep the static stride (pulled, synth10k /
-  // weights measured no better: balanced waves all join the scan at once at the end)
-  constexpr bool kPull = !EXACT;
+  // the chunks cover order[0, end of the last chunk): scan in that order when it lists every pass
+  const int32_t* sorder = (n_chunk > 0 && sld(chunk_tab + 3 * (n_chunk - 1) + 1) == A.n_pass) ? order : nullptr;
+  // covered-span scan (the host checked window layout and alignment): every pass's slices are loaded by the
+  // correlation only when the chunks list every pass
+  const bool span = EXACT && Fused<E>::v && span_req && sorder && !S.tab;
+  if constexpr (Fused<E>::v) {
+    if (span) eng.vflag = vflag;
+  }
+  // the padded engines' correlation waves pull row tasks (w = 499: fused launch 4.80 -> 3.99 ms, their task costs vary
+  // with the pivot-slice table's coverage), from per-XCD counters when the launch has them (xq); the exact ones keep
+  // the static stride (pulled, synth10k / weights measured no better: balanced waves all join the scan at once)
+  TaskSource src;
+  src.stride = (int64_t)gridDim.x * kFft;
+  if constexpr (!EXACT) {
+    src.q = xq ? xq : counter + 1;
+    src.xcd = xq != nullptr;
+  }
   if (wave < kFft) {
     __builtin_amdgcn_s_setprio(kCorrPrio);  // correlation waves issue first when both are ready
     stack_tasks<E, EXACT>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
-                          (int64_t)gridDim.x * kFft, kPull ? counter + 1 : nullptr);
+                          src);
     __builtin_amdgcn_s_setprio(0);
   }
-  // the chunks cover order[0, end of the last chunk): scan in that order when it lists every pass
-  const int32_t* sorder = (n_chunk > 0 && sld(chunk_tab + 3 * (n_chunk - 1) + 1) == A.n_pass) ? order : nullptr;
-  scan_units<kDepth>(A, S, vflag, counter, lane, sorder);
+  scan_units<kDepth>(A, S, vflag, counter, lane, sorder, span);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
@@ -1082,6 +1222,11 @@ template <class E>
 static int64_t table_bytes(int64_t n_pass) {
   return n_pass * (tab_pass_f2<E::kTabBins>() * (int64_t)sizeof(float2) + 2 * kTabEnt * (int64_t)sizeof(int32_t));
 }
+// the stack workspace: the pivot-slice table, then 8 per-XCD task counters of the validated launch
+constexpr int64_t kXcdQBytes = 64;
+static int64_t stack_ws_bytes(int n, int64_t n_pass) {
+  return (n == 500 ? table_bytes<EngF500>(n_pass) : table_bytes<EngP1024>(n_pass)) + kXcdQBytes;
+}
 
 static int launch_table(VsgArgs& A, int n, float2* tab, hipStream_t s) {
   const int grid = (int)std::min<int64_t>(((int64_t)A.n_pass + 3) / 4, 8 * (int64_t)cu_count());
@@ -1098,7 +1243,7 @@ DVH_API int64_t dvh_vsg_stack_workspace(int32_t n_pass, int32_t w) {
   bool pad;
   const int n = choose_fft(w, &pad);
   if (n_pass <= 0 || !table_engine(n)) return 0;
-  return n == 500 ? table_bytes<EngF500>(n_pass) : table_bytes<EngP1024>(n_pass);
+  return stack_ws_bytes(n, n_pass);
 }
 
 DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_stride, int32_t n_pass,
@@ -1125,6 +1270,17 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   float2* tab = (table_engine(n) && spec_ws) ? reinterpret_cast<float2*>(spec_ws) : nullptr;
   hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t) * ((size_t)S.n_win + 2), s);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
+  static const bool xcd_env = !getenv("DVH_VSTACK_XCDQ") || atoi(getenv("DVH_VSTACK_XCDQ")) != 0;  // A/B
+  uint32_t* xq = (tab && xcd_env) ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(spec_ws) +
+                                                                stack_ws_bytes(n, n_pass) - kXcdQBytes)
+                                  : nullptr;
+  if (xq && (e = hipMemsetAsync(xq, 0, kXcdQBytes, s)) != hipSuccess) return set_error(-3, hipGetErrorString(e));
+  // the covered-span scan: w = 500's fused engine, default windows, 16-byte aligned rows (the kernel also needs the
+  // chunks to list every pass, and falls back to the whole-window scan otherwise)
+  static const int span_env = getenv("DVH_SCAN_SPAN") ? atoi(getenv("DVH_SCAN_SPAN")) : 0;  // A/B
+  int32_t span = (span_env && n == 500 && !scan_tab && n_t % 4 == 0 && ch_stride % 4 == 0 && pass_stride % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(win) % 16 == 0 &&
+                  ((int64_t)(n_ch - 1) * ch_stride + n_t) * 4 < 0xfffffff0LL) ? 1 : 0;
   if (tab)
     if (int rc = launch_table(A, n, tab, s)) return rc;
   const int64_t tasks = (int64_t)n_chunk * R;
@@ -1132,8 +1288,13 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   if (get_vstack(n, &v)) {
     const int64_t need = (tasks + v.fft - 1) / v.fft;
     const int grid = (int)(need < v.bpc * cu_count() ? (need > 0 ? need : 1) : v.bpc * cu_count());
-    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &tab};
+    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &tab, &xq,
+                    &span};
     if (int rc = launch(v.fn, grid, v.fft + v.scan, v.lds, args, s)) return rc;
+    if (span && S.n_win > 0) {  // the windows the covered-span scan could not decide, rescanned whole
+      hipLaunchKernelGGL(window_fixup_kernel, dim3((unsigned)S.n_win), dim3(256), 0, s, A, S, vflag);
+      if ((e = hipGetLastError()) != hipSuccess) return set_error(-3, hipGetErrorString(e));
+    }
   } else {  // no fused form: the scan as its own launch, then the plain stack launch
     void* sargs[] = {&A, (void*)&S, &vflag, &counter};
     if (int rc = launch((const void*)window_scan_kernel, 4 * cu_count(), 4, 0, sargs, s)) return rc;

@@ -114,6 +114,10 @@ __device__ __forceinline__ int opaque(int v) {
 __device__ __forceinline__ uint32_t nzbits(float x) { return __builtin_bit_cast(uint32_t, x) & 0x7fffffffu; }
 // OR-accumulated non-zero bits of the loaded samples (one v_and_or per sample)
 __device__ __forceinline__ uint32_t maxbits(uint32_t b, float x) { return b | nzbits(x); }
+// Validity flags of the covered-span scan (dvh_vsg.hip): per pass the max |x| bit pattern of the samples the scan
+// read (>= kInfBits: a NaN / inf), or'ed with kSuspect when a correlation wave saw a non-finite spectrum it cannot
+// attribute to one pass (the window is then rescanned whole).
+constexpr uint32_t kInfBits = 0x7f800000u, kSuspect = 0x80000000u;
 
 __device__ __forceinline__ void accumulate_cross(float2 Az, float2 Bc, float2& C) {
   // P = (A + B) / 2, R = (A - B) / 2i with B = conj(Bc)  ->  P conj(R) = (i / 4) (A + B) conj(A - B)
@@ -321,6 +325,8 @@ struct FusedOps {
   bool live_f, live_o;
   const float2* tab = nullptr;  // the pass table of pivot spectra (stack kernels), or none
   int w;                        // sub-window length: the padded engines load samples n < w
+  uint32_t* vflag = nullptr;    // validated launch with the covered-span scan: the passes' validity flags, to which
+                                // the correlation reports the non-finite samples it loads (the scan leaves them out)
 
   __device__ FusedOps(char* lds, int wave, int lane_, int w_) : lane(lane_), live_f(false), live_o(false), w(w_) {
     tw = reinterpret_cast<float2*>(lds);
@@ -335,6 +341,28 @@ struct FusedOps {
   // the stages after stage 1 of the transform whose stage-1 output is in bufB; cross spectra into C
   __device__ __forceinline__ void finish(float2 (&C)[kNH]) const {
     self().finish_with([&](int j, float2 a, float2 b) { accumulate_cross(a, b, C[j]); });
+  }
+
+  // Covered-span scan: a loaded sub-window that is not transformed (a zero pivot or receiver slice) is checked here
+  // for non-finite samples (rare); a transformed one carries them into the accumulated spectra, which the stack
+  // tasks test.  p2 < 0: both halves of z belong to pass p; else the real half to p, the imaginary half to p2.
+  __device__ void check_untransformed(const float2 (&z)[kNJ], int p, int p2 = -1) const {
+    if (!vflag) return;
+    uint32_t ma = 0, mb = 0;
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j) {
+      ma = max(ma, nzbits(z[j].x));
+      mb = max(mb, nzbits(z[j].y));
+    }
+    const bool ba = __ballot(ma >= kInfBits) != 0, bb = __ballot(mb >= kInfBits) != 0;
+    if (lane == 0) {
+      if (p2 < 0) {
+        if (ba || bb) atomicMax(vflag + p, kInfBits);
+      } else {
+        if (ba) atomicMax(vflag + p, kInfBits);
+        if (bb) atomicMax(vflag + p2, kInfBits);
+      }
+    }
   }
 
   // the pass's table entries hold all its sub-windows (head nwin of entry 0 >= 0)
@@ -365,6 +393,7 @@ struct FusedOps {
       }
       const bool live = (__ballot(bp != 0) != 0) && (__ballot(br != 0) != 0);
       if (live) self().stage1(z);
+      else check_untransformed(z, t.p);
       if (q + 1 < nq) load(t, start(q + 1), z);
       if (!live) continue;  // exactly zero in the reference
       if (q < t.nwin_f) {
@@ -456,6 +485,7 @@ struct FusedOps {
       }
       const bool live = pairjob ? (la || lb) : (nzp && nzr);
       if (live) self().stage1(z);
+      else check_untransformed(z, t.p);
       if (k + 1 < nj) tab_load(t, J, k + 1, hop, z);
       if (!live) continue;
       if (pairjob) {
@@ -603,6 +633,8 @@ struct FusedOps {
       const bool lb = hb && (__ballot(br != 0) != 0) && sld(&Pb[BINS - 1].x) != 0.f;
       const bool live = la || lb;
       if (live) self().stage1(z);
+      else check_untransformed(z, __builtin_amdgcn_readlane(p, (2 * jb) / W),
+                               hb ? __builtin_amdgcn_readlane(p, (2 * jb + 1) / W) : __builtin_amdgcn_readlane(p, (2 * jb) / W));
       const float2 *Pa_c = Pa, *Pb_c = Pb;
       const float wa_c = wa, wb_c = wb;
       if (jb + 1 < nj) {  // the next pair's samples, loaded under this transform
@@ -636,6 +668,12 @@ struct FusedOps {
           U[j].y += wb_c * (pb[j].y * r.x - pb[j].x * r.y);
         }
       });
+    }
+    if (vflag) {  // a non-finite sample of some pass reached U: each of the task's passes is rescanned whole
+      bool nf = false;
+#pragma unroll
+      for (int j = 0; j < NH_; ++j) nf |= !isfinite(U[j].x) || !isfinite(U[j].y);
+      if (__ballot(nf) != 0 && act) atomicOr(vflag + p, kSuspect);
     }
     if constexpr (RAMP) {
       // Gh = (-1)^lane (conj on the shared window) U conj(tw[f])

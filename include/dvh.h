@@ -119,8 +119,9 @@ int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_st
 /* Bytes of the spec_ws workspace dvh_vsg_stack / dvh_vsg_stack_validated take for n_pass passes at
  * window length w: the spectra of every pass's pivot slices that many rows share (w = 500: the shared
  * windows of both sides and the far rows' clamped windows, 24 KiB + 32 B per pass), which lets the
- * stack launch transform only receivers for those rows (EngF500::spectra_tab).  0 when w does not use
- * it; with spec_ws == NULL the stack entries run the per-sub-window engine instead. */
+ * stack launch transform only receivers for those rows (EngF500::spectra_tab), and 64 bytes of per-XCD task
+ * counters for dvh_vsg_stack_validated.  0 when w does not use it; with spec_ws == NULL the stack entries run the
+ * per-sub-window engine instead. */
 int64_t dvh_vsg_stack_workspace(int32_t n_pass, int32_t w);
 
 /* ---------------------------------------------------------------- dispersion (map_fv)
