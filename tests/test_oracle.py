@@ -192,3 +192,43 @@ def test_oracle_window_selection_matches_reference(case):
     if vx:
         assert np.array_equal(np.concatenate([v[0] for v in vx]), g[case + "_vx"])
         assert np.array_equal(np.concatenate([v[1] for v in vx]), g[case + "_vt"])
+
+
+def test_oracle_daily_xcorr_workflow_matches_reference():
+    """The xcorr flavour of the daily workflow restated with the oracle (apis/imaging_workflow.py:33-80, 199-201):
+    per record the xcorr preprocessing, the window selection, VirtualShotGather per window (norm=False, two-sided)
+    and the class mean; the day's image as the sum of per-record means, against tests/golden/workflow.npz; then
+    compute_disp_image() with its defaults (whole gather, norm=False)."""
+    from oracle import disp as odisp
+    from oracle import preprocess as op
+    from oracle import select as osel
+    from oracle import vsg as ovsg
+    g = gio.load("workflow")
+    day = None
+    for k, c in enumerate(gio.workflow_files()):
+        t_axis = c["t_axis"]
+        d = op.surface_wave_prep(c["rec"], t_axis[1] - t_axis[0], method="xcorr", scipy_filter=True)
+        dist = (c["x_axis"] - 400) * 8.16
+        wins = osel.locate_windows(t_axis.size, t_axis, dist, c["x0"], c["start_x_tracking"], c["veh_states"],
+                                   c["t_trk"], t_axis[1] - t_axis[0], **c["select_kw"])
+        assert len(wins) == int(g[f"n_windows_{k}"])
+        kw = dict(c["imaging_kw"])
+        other = kw.pop("include_other_side")
+        gathers = []
+        for kv, sx, ex, st, et in wins:
+            vx, vt = osel.veh_state_xt(c["veh_states"][kv], c["start_x_tracking"], c["dist_trk"], c["t_trk"])
+            w = dict(data=d[sx:ex, st:et], x_axis=dist[sx:ex], t_axis=t_axis[st:et], veh_state_x=vx, veh_state_t=vt)
+            gathers.append(ovsg.virtual_shot_gather(w, include_other_side=other, norm=False, **kw))
+        assert [x[0].shape[-1] for x in gathers] == list(g[f"w_{k}"])
+        mean = ovsg.stack([x[0] for x in gathers])
+        assert np.abs(mean - g[f"file_avg_{k}"]).max() <= 1e-9 * np.abs(g[f"file_avg_{k}"]).max()
+        if day is None:
+            day, gx, gt = mean, gathers[0][1], gathers[0][2]
+        else:
+            n = min(day.shape[-1], mean.shape[-1])
+            day = day.copy()
+            day[:, :n] += mean[:, :n]
+    assert np.abs(day - g["day_xcf"]).max() <= 1e-9 * np.abs(g["day_xcf"]).max()
+    assert np.array_equal(gx, g["day_x_axis"]) and np.array_equal(gt, g["day_t_axis"])
+    fv = odisp.compute_disp_image(day, gx, gt)
+    assert np.abs(fv - g["day_fv"]).max() <= 1e-6 * np.abs(g["day_fv"]).max()
