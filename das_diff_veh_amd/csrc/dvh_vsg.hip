@@ -556,6 +556,9 @@ __device__ __forceinline__ void stackp_tasks(E& eng, const VsgArgs& A, const flo
       }
       const bool bad = __ballot(isnan(af + ao)) != 0;
       const bool nzo = other && eng.live_o && (__ballot(ao != 0.f) != 0);
+      if constexpr (Fused<E>::v) {  // covered-span scan: a non-finite sample among this pass's loaded slices
+        if (eng.vflag && __ballot(!isfinite(af + ao)) != 0 && lane_ == 0) atomicMax(eng.vflag + p, kInfBits);
+      }
       float ff = task.nwin_f > 0 ? 1.0f / (float)task.nwin_f : 0.f;
       float fo = task.nwin_o > 0 ? 1.0f / (float)task.nwin_o : 0.f;
       side_scale(A.flags, task, sf, so, ff, fo);
@@ -963,7 +966,7 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
   const int32_t* sorder = (n_chunk > 0 && sld(chunk_tab + 3 * (n_chunk - 1) + 1) == A.n_pass) ? order : nullptr;
   // covered-span scan (the host checked window layout and alignment): every pass's slices are loaded by the
   // correlation only when the chunks list every pass
-  const bool span = EXACT && Fused<E>::v && span_req && sorder && !S.tab;
+  const bool span = Fused<E>::v && span_req && sorder && !S.tab;
   if constexpr (Fused<E>::v) {
     if (span) eng.vflag = vflag;
   }
@@ -1275,10 +1278,10 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
                                                                 stack_ws_bytes(n, n_pass) - kXcdQBytes)
                                   : nullptr;
   if (xq && (e = hipMemsetAsync(xq, 0, kXcdQBytes, s)) != hipSuccess) return set_error(-3, hipGetErrorString(e));
-  // the covered-span scan: w = 500's fused engine, default windows, 16-byte aligned rows (the kernel also needs the
-  // chunks to list every pass, and falls back to the whole-window scan otherwise)
+  // the covered-span scan: the fused engines (w = 500, padded 1 024), default windows, 16-byte aligned rows (the
+  // kernel also needs the chunks to list every pass, and falls back to the whole-window scan otherwise)
   static const int span_env = getenv("DVH_SCAN_SPAN") ? atoi(getenv("DVH_SCAN_SPAN")) : 0;  // A/B
-  int32_t span = (span_env && n == 500 && !scan_tab && n_t % 4 == 0 && ch_stride % 4 == 0 && pass_stride % 4 == 0 &&
+  int32_t span = (span_env && (n == 500 || n == 1024) && !scan_tab && n_t % 4 == 0 && ch_stride % 4 == 0 && pass_stride % 4 == 0 &&
                   reinterpret_cast<uintptr_t>(win) % 16 == 0 &&
                   ((int64_t)(n_ch - 1) * ch_stride + n_t) * 4 < 0xfffffff0LL) ? 1 : 0;
   if (tab)
