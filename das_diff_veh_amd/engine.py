@@ -222,8 +222,18 @@ def _stacked(windows, prm, slots, n_slot, device, chunk, counts):
             early = _stage(windows, range(len(windows)), device)
             stagings.append(early)
         groups, axes = _groups(windows, prm)
-        if len({key[1:3] for key in groups}) != 1:
+        if len({key[1] for key in groups}) != 1:
             raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
+        # Windows whose time steps round to different w (499 / 500 on real axes) may share a class: sum(images)
+        # keeps the first image's lag axis and adds the others' first min(w) lags (VirtualShotGather.__add__,
+        # apis/virtual_shot_gather.py:195-199).  The stacks of the other lengths are formed apart and added so.
+        w_of = {i: key[2] for key, idx in groups.items() for i in idx}
+        first_w = {}
+        for i, s in enumerate(slots):
+            first_w.setdefault(int(s), w_of[i])
+        if len(set(first_w.values())) > 1:
+            raise ValueError("classes whose first passes have different lag lengths w: stack them in separate calls")
+        w0 = next(iter(first_w.values()), None)
         if early is not None:
             memo = {}
             staged = [(idx, key, _rows_of(early, idx, len(windows), memo)) for key, idx in groups.items()]
@@ -238,7 +248,15 @@ def _stacked(windows, prm, slots, n_slot, device, chunk, counts):
             data = data_fn()
             sched = StackSchedule(slots[idx], n_slot, chunk=chunk, counts=counts)
             fn = vsg_stack_validated if plan.flags & 6 else vsg_stack
-            out = fn(data, plan, sched, out=out, accumulate=out is not None)
+            if key[2] == w0:
+                out = fn(data, plan, sched, out=out, accumulate=out is not None)
+            else:
+                import torch
+                part = fn(data, plan, sched)
+                if out is None:
+                    out = torch.zeros((n_slot, key[1], w0), dtype=torch.float32, device=part.device)
+                m = min(w0, key[2])
+                out[:, :, :m] += part[:, :, :m]
         return out, axes
     except BaseException:
         # a validation error after the copies started (geometry, shapes, trajectories): the background copies
@@ -261,8 +279,10 @@ def stacked_sharded(windows, prm: VsgParams, slots=None, n_slot=1, group=None, d
     device = device or default_device()
     slots = np.zeros(len(windows), dtype=np.int64) if slots is None else np.asarray(slots, dtype=np.int64)
     keys, axes = zip(*[_axes(w, prm) for w in windows]) if windows else ((), ())
-    if len({k[:2] for k in keys}) != 1:
+    if len({k[0] for k in keys}) != 1:
         raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
+    if len({k[1] for k in keys}) != 1:
+        raise ValueError("the sharded class means need one lag length w (stacked() takes mixed ones)")
     # every pass is checked on every rank before sharding, so a bad pass raises the same error everywhere
     # instead of only on its owner (distributed.sharded_class_means also shares any error a rank hits)
     failed, _ = pass_failures(windows, prm)
@@ -286,8 +306,9 @@ def pass_failures(windows, prm: VsgParams):
     """Per-pass failure status of a batch, decided on the host before any launch (skip +
     count): {pass index: reason} for a gather geometry preprocessing_window cannot slice, the
     dt == 0.004 window-length mismatch, a trajectory interp1d (and dvh_pass_geometry) would reject
-    (< 2 distinct finite tracked points), or a gather shape other than the batch's (that of its first
-    good pass).  Also returns every pass's GatherAxes (None for a failed one)."""
+    (< 2 distinct finite tracked points), or a gather row count other than the batch's (that of its first
+    good pass; another lag length w stacks as the reference's sum does).  Also returns every pass's GatherAxes
+    (None for a failed one)."""
     failed, keys, axes = {}, {}, [None] * len(windows)
     for i, w in enumerate(windows):
         try:
@@ -299,11 +320,11 @@ def pass_failures(windows, prm: VsgParams):
         if vx.size < 2 or vx.size != vt.size or not np.all(np.isfinite(vx)) or np.unique(vx).size != vx.size:
             failed[i] = "trajectory needs >= 2 distinct finite tracked points (interp1d)"
     ok = [i for i in range(len(windows)) if i not in failed]
-    if ok:
-        rw = keys[ok[0]][:2]
+    if ok:  # gathers of another lag length w stack as sum(images) does; another row count cannot
+        r0 = keys[ok[0]][0]
         for i in ok:
-            if keys[i][:2] != rw:
-                failed[i] = f"gather shape (R, w) = {keys[i][:2]} differs from the batch's {rw}"
+            if keys[i][0] != r0:
+                failed[i] = f"gather rows R = {keys[i][0]} differ from the batch's {r0}"
     for i in failed:
         axes[i] = None
     return failed, axes
