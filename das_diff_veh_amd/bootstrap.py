@@ -118,8 +118,14 @@ def _side_stream(device, k):
 
 
 class GatherCache:
-    """Per-pass gathers [n, R, w] of a window list on the device, computed once
-    (VirtualShotGathersFromWindows.get_images' per-pass images: norm=False, two-sided)."""
+    """Per-pass gathers [n, R, W] of a window list on the device, computed once
+    (VirtualShotGathersFromWindows.get_images' per-pass images: norm=False, two-sided).
+
+    Windows whose time steps round to different lag lengths w (499 / 500 on real axes) share the cache: every
+    gather sits zero-padded to the widest W, so that a resample's sum over the padded rows is the reference's
+    sum(images) -- VirtualShotGather.__add__ adds the other images' first min(w) lags to the first image's
+    (apis/virtual_shot_gather.py:195-199) -- on the first drawn pass's lag axis, whose width and time step its
+    dispersion image then takes (compute_disp_image, :247-258)."""
 
     def __init__(self, windows, pivot, start_x, end_x, wlen=2, include_other_side=True, device=None):
         self.device = device or default_device()
@@ -130,10 +136,29 @@ class GatherCache:
         if len(shapes) != 1:
             raise ValueError("bootstrap windows must share one shape")
         n_ch, n_t = shapes.pop()
-        self.plan = VsgPlan(geoms, self.prm, n_ch, n_t)
-        data = to_device_f32([w.data for w in windows], self.device)
-        self.G = vsg_gathers(data, self.plan)  # [n, R, w]
+        self.w_of = np.array([g.w for g in geoms], dtype=np.int64)
+        by_w = {}
+        for i, g in enumerate(geoms):
+            by_w.setdefault(g.w, []).append(i)
+        if len(by_w) == 1:
+            self.plan = VsgPlan(geoms, self.prm, n_ch, n_t)
+            self.G = vsg_gathers(to_device_f32([w.data for w in windows], self.device), self.plan)  # [n, R, w]
+        else:
+            plans = {w: VsgPlan([geoms[i] for i in idx], self.prm, n_ch, n_t) for w, idx in by_w.items()}
+            if len({p.R for p in plans.values()}) != 1:
+                raise ValueError("operands could not be broadcast together: passes produce gathers of different shapes")
+            self.plan = plans[geoms[0].w]
+            W = max(by_w)
+            self.G = torch.zeros((len(windows), self.plan.R, W), dtype=torch.float32, device=self.device)
+            for w, idx in by_w.items():
+                g = vsg_gathers(to_device_f32([windows[i].data for i in idx], self.device), plans[w])
+                self.G[torch.as_tensor(idx, device=self.device), :, :w] = g
+        self.W = int(self.G.shape[-1])
         self.gx, self.gt = geoms[0].gather_x_axis, geoms[0].gather_t_axis
+        # per lag length: the time axis of its first pass (a resample's image takes its first drawn pass's)
+        self._gt_of = {}
+        for g in geoms:
+            self._gt_of.setdefault(g.w, g.gather_t_axis)
         self.n = len(windows)
         self._disp = {}
 
@@ -156,26 +181,50 @@ class GatherCache:
         self.gx = x_axis[st:st + self.plan.R] - x_axis[pv]
         self.gt = (np.arange(self.plan.w) - self.plan.w // 2) * dt
         self.n = data.shape[0]
+        self.w_of = np.full(self.n, self.plan.w, dtype=np.int64)
+        self.W = self.plan.w
+        self._gt_of = {self.plan.w: self.gt}
         self._disp = {}
         return self
 
-    def disp_plan(self, start_x=-150, end_x=0, freqs=FREQS, vels=VELS):
-        """compute_disp_image's nearest-offset channel slice and its DispPlan (dx = 8.16, :247-258)."""
+    def disp_plan(self, start_x=-150, end_x=0, freqs=FREQS, vels=VELS, w=None):
+        """compute_disp_image's nearest-offset channel slice and its DispPlan (dx = 8.16, :247-258) for the images
+        of lag length w (default: the first pass's)."""
+        w = int(self.w_of[0]) if w is None else int(w)
         s = int(np.abs(self.gx - start_x).argmin())
         e = int(np.abs(self.gx - end_x).argmin())
-        key = (s, e, id(freqs), id(vels))
+        key = (s, e, id(freqs), id(vels), w)
         if key not in self._disp:
-            dt = float(self.gt[1] - self.gt[0])
+            gt = self._gt_of[w]
+            dt = float(gt[1] - gt[0])
             # plans are shared across caches of one geometry (a convergence test per class builds a new cache;
             # the plan's host tables and their device copies are the same)
-            pkey = (e + 1 - s, self.plan.w, dt, np.asarray(freqs, dtype=np.float64).tobytes(),
+            pkey = (e + 1 - s, w, dt, np.asarray(freqs, dtype=np.float64).tobytes(),
                     np.asarray(vels, dtype=np.float64).tobytes())
             if pkey not in _DISP_PLANS:
                 if len(_DISP_PLANS) >= 16:
                     _DISP_PLANS.pop(next(iter(_DISP_PLANS)))
-                _DISP_PLANS[pkey] = DispPlan(e + 1 - s, self.plan.w, 8.16, dt, freqs, vels)
+                _DISP_PLANS[pkey] = DispPlan(e + 1 - s, w, 8.16, dt, freqs, vels)
             self._disp[key] = (s, e, _DISP_PLANS[pkey])
         return self._disp[key]
+
+    def images_of(self, stacks, first, start_x=-150, end_x=0):
+        """f-v images [B, Nvel, Nfreq] of resample stacks [B, nch, W] whose first drawn passes are ``first``: each
+        on its first pass's lag axis (its width w and time step)."""
+        wf = self.w_of[np.asarray(first, dtype=np.int64)]
+        if np.all(wf == self.W):
+            _, _, plan = self.disp_plan(start_x, end_x, w=self.W)
+            return fv_from_fk(fk_grid(stacks, plan), plan)
+        out = None
+        for w in np.unique(wf):
+            rows = np.flatnonzero(wf == w)
+            _, _, plan = self.disp_plan(start_x, end_x, w=int(w))
+            rt = torch.as_tensor(rows, device=self.device)
+            fv = fv_from_fk(fk_grid(stacks[rt][:, :, :int(w)], plan), plan)
+            if out is None:
+                out = torch.empty((stacks.shape[0],) + tuple(fv.shape[1:]), dtype=fv.dtype, device=fv.device)
+            out[rt] = fv
+        return out
 
     def resample_stacks(self, sel, start_x=-150, end_x=0, out=None):
         """Mean gathers over the disp rows for every draw: sel [B, k] pass indices -> [B, nch, w] (into
@@ -184,7 +233,7 @@ class GatherCache:
         if sel.ndim != 2 or sel.size == 0 or sel.min() < 0 or sel.max() >= self.n:
             raise ValueError("selections must be [B, k] pass indices")
         s, e, _ = self.disp_plan(start_x, end_x)
-        w, R = self.plan.w, self.plan.R
+        w, R = self.W, self.plan.R
         B, k = sel.shape
         if out is None:
             out = torch.empty((B, e + 1 - s, w), dtype=torch.float32, device=self.device)
@@ -211,7 +260,7 @@ class GatherCache:
         if flat.min() < 0 or flat.max() >= self.n:
             raise ValueError("selections must be [B, k] pass indices")
         s, e, _ = self.disp_plan(start_x, end_x)
-        w, R = self.plan.w, self.plan.R
+        w, R = self.W, self.plan.R
         B = sum(x.shape[0] for x in sels)
         rows = (e + 1 - s) * w
         if out is None:
@@ -231,8 +280,8 @@ class GatherCache:
 
     def resample_images(self, sel, start_x=-150, end_x=0):
         """f-v images [B, Nvel, Nfreq] of every draw's stack (compute_disp_image(end_x, start_x))."""
-        _, _, plan = self.disp_plan(start_x, end_x)
-        return fv_from_fk(fk_grid(self.resample_stacks(sel, start_x, end_x), plan), plan)
+        sel = np.asarray(sel, dtype=np.int32)
+        return self.images_of(self.resample_stacks(sel, start_x, end_x), sel[:, 0], start_x, end_x)
 
 
 def bootstrap_ridges(cache: GatherCache, sels, sigma, ref_freq_idx, freq_lb, freq_up, ref_vel, start_x=-150,
@@ -260,14 +309,13 @@ def convergence(cache: GatherCache, max_size, bt_times, sigma, ref_freq_idx, fre
     sels = draw_sizes(cache.n, range(1, max_size + 1), bt_times, rand)
     if phases is not None:
         phases["draw_host_s"] = time.perf_counter() - t_draw
-    s, e, plan = cache.disp_plan(start_x, end_x)
     B = max_size * bt_times
     ev = (lambda name: phases.setdefault(name, torch.cuda.Event(enable_timing=True)).record()) if phases is not None \
         else (lambda name: None)
     ev("select0")
     stacks = cache.resample_stacks_sizes(sels, start_x, end_x)
     ev("select1")
-    fv = fv_from_fk(fk_grid(stacks, plan), plan)
+    fv = cache.images_of(stacks, np.concatenate([x[:, 0] for x in sels]), start_x, end_x)
     ev("disp1")
     out = np.empty((len(freq_lb), max_size))
     # every mode's walk queued at once, each on its own stream: one walk is one wave per resample (1 800 waves,

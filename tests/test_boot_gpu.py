@@ -271,3 +271,62 @@ def test_convergence_test_small(device):
                 assert abs(np.sum(np.std(np.stack(ref_sm), axis=0)) - got[m, k - 1]) <= 1e-9
     n_near = _audit_report("convergence_test", audits, fv_err)
     assert n_near <= 4, n_near
+
+
+def _mixed_windows():
+    """The w = 500 and w = 499 fixtures' passes interleaved (one 56 x 4 096 shape): real records mix both lag lengths
+    (int(wlen / dt) of each window's own time step, apis/virtual_shot_gather.py:18,41)."""
+    from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
+    g5, g9 = gio.load("vsg_w500"), gio.load("vsg_w499")
+    srcs = [(g5, 0), (g9, 0), (g5, 1), (g5, 2), (g9, 1), (g5, 3), (g5, 4)]
+    wins = [SurfaceWaveWindow(**gio.pass_arrays(g, i)) for g, i in srcs]
+    ow = [gio.oracle_window(g, i) for g, i in srcs]
+    return wins, ow
+
+
+def test_mixed_lag_lengths_resample_images(device):
+    """A gather cache over windows of w = 500 and 499: each resample's stack is the reference's sum(images) on its
+    first drawn pass's lag axis (VirtualShotGather.__add__ truncating the others, apis/virtual_shot_gather.py:195-199)
+    and its f-v image is compute_disp_image on that axis -- against the oracle (oracle.vsg.stack, oracle.disp), for
+    draws led by either length, within 1e-4, picks on the reference maximum."""
+    from das_diff_veh_amd import bootstrap as bt
+    from oracle import disp as odisp
+    from oracle import vsg as ovsg
+    wins, ow = _mixed_windows()
+    og = [ovsg.virtual_shot_gather(w, include_other_side=True, norm=False, **KW, wlen=2) for w in ow]
+    assert {x[0].shape[-1] for x in og} == {499, 500}
+    cache = bt.GatherCache(wins, **KW)
+    sels = np.array([[1, 2, 3], [2, 1, 4], [4, 6, 1], [3, 5, 2], [6, 1, 1]], dtype=np.int32)
+    fv = cache.resample_images(sels).cpu().numpy()
+    for b, sel in enumerate(sels):
+        ref = ovsg.stack([og[i][0] for i in sel])
+        rfv = odisp.compute_disp_image(ref, og[sel[0]][1], og[sel[0]][2], start_x=-150, end_x=0)
+        assert np.abs(fv[b] - rfv).max() <= 1e-4 * np.abs(rfv).max(), b
+        _image_picks_rule(fv[b], rfv)
+
+
+def test_mixed_lag_lengths_bootstrap_and_convergence(device):
+    """bootstrap_disp and convergence_test over the mixed windows: the reference's draws (random.seed), every
+    resample's ridges equal the walk of the oracle on our own images (1e-9), and the images match the oracle's."""
+    from das_diff_veh_amd import bootstrap as bt
+    from das_diff_veh_amd.apis.imaging_classes import bootstrap_disp, convergence_test
+    from oracle import ridge as orid
+    wins, ow = _mixed_windows()
+    g = gio.load("ridge")
+    mode1 = _mode1(g)
+    args = ([25, 50], 700, 500, 900, [80, 130], [2.5, 10], [14, 15], [None, mode1])
+    random.seed(3)
+    rv, fq = bootstrap_disp(wins, 3, 6, *args)
+    random.seed(3)
+    sels = bt.draw(len(wins), 3, 6)
+    assert len({int(bt.GatherCache(wins, **KW).w_of[s[0]]) for s in sels}) == 2  # draws led by both lengths
+    fv = bt.GatherCache(wins, **KW).resample_images(sels).cpu().numpy()
+    for b in range(6):
+        for m, (lb, ub, ri, sg, vr) in enumerate(((2.5, 14, 80, 25, None), (10, 15, 130, 50, mode1))):
+            band = (fq >= lb) & (fq < ub)
+            o = orid.extract_ridge_ref_idx(fq[band], bt.VELS, fv[b][:, band], ref_freq_idx=ri - int(np.sum(fq < lb)),
+                                           sigma=sg, vel_max=800, ref_vel=vr)
+            np.testing.assert_allclose(rv[m][b], o, rtol=0, atol=1e-9)
+    random.seed(4)
+    got = convergence_test(2, wins, 3, *args)
+    assert got.shape == (2, 2) and np.all(np.isfinite(got))
