@@ -127,29 +127,15 @@ __device__ __forceinline__ int xcd_block() {
   return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
 }
 
-// The row tasks [0, n) of a stack launch as one wave takes them: a static stride (t0, t0 + stride, ...), pulled from
-// one global counter, or pulled from eight per-XCD counters -- XCD x first drains its own contiguous eighth of the
-// tasks, then the other XCDs' leftovers -- so that the row tasks of a chunk, which read the chunk's windows and pivot
-// tables, run in one XCD's L2 while the waves stay balanced.
+// The row tasks [0, n) of a stack launch as one wave takes them: a static stride (t0, t0 + stride, ...), or pulled
+// from a global counter.  (Eight per-XCD counters, each XCD draining its own eighth of the tasks before the others'
+// leftovers, measured no faster on the padded engine: w = 499 synth10k launch 15.05 vs 14.99 ms, weights 1.80-1.83
+// vs 1.81-1.83 ms.)
 struct TaskSource {
-  uint32_t* q = nullptr;  // nullptr: static stride; else one counter, or 8 per-XCD counters (xcd)
-  bool xcd = false;
+  uint32_t* q = nullptr;  // nullptr: static stride
   int64_t n = 0, stride = 1;
-  int cur = 0;  // per-XCD: queues tried so far (wave-uniform)
-  __device__ int64_t pull(int lane) {
-    if (!xcd) return pull_unit(q, lane);
-    const int x = blockIdx.x & 7;  // workgroups are dealt round robin over the 8 XCDs
-    while (cur < 8) {
-      const int y = (x + cur) & 7;
-      const int64_t b = n * y / 8, e = n * (y + 1) / 8;
-      const int64_t t = b + pull_unit(q + y, lane);
-      if (t < e) return t;
-      ++cur;
-    }
-    return n;
-  }
-  __device__ int64_t first(int64_t t0, int lane) { return q ? pull(lane) : t0; }
-  __device__ int64_t next(int64_t t, int lane) { return q ? pull(lane) : t + stride; }
+  __device__ int64_t first(int64_t t0, int lane) { return q ? pull_unit(q, lane) : t0; }
+  __device__ int64_t next(int64_t t, int lane) { return q ? pull_unit(q, lane) : t + stride; }
 };
 
 template <class E>
@@ -957,7 +943,7 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
     const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
     float* __restrict__ stack, ScanArgs S, uint32_t* __restrict__ vflag, uint32_t* __restrict__ counter,
-    const float2* __restrict__ ptab, uint32_t* __restrict__ xq, int32_t span_req) {
+    const float2* __restrict__ ptab, int32_t span_req) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   E eng = make_engine<E>(lds);
   bind_engine(eng, A, ptab);
@@ -971,14 +957,11 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     if (span) eng.vflag = vflag;
   }
   // the padded engines' correlation waves pull row tasks (w = 499: fused launch 4.80 -> 3.99 ms, their task costs vary
-  // with the pivot-slice table's coverage), from per-XCD counters when the launch has them (xq); the exact ones keep
-  // the static stride (pulled, synth10k / weights measured no better: balanced waves all join the scan at once)
+  // with the pivot-slice table's coverage); the exact ones keep the static stride (pulled, synth10k / weights measured
+  // no better: balanced waves all join the scan at once)
   TaskSource src;
   src.stride = (int64_t)gridDim.x * kFft;
-  if constexpr (!EXACT) {
-    src.q = xq ? xq : counter + 1;
-    src.xcd = xq != nullptr;
-  }
+  if constexpr (!EXACT) src.q = counter + 1;
   if (wave < kFft) {
     __builtin_amdgcn_s_setprio(kCorrPrio);  // correlation waves issue first when both are ready
     stack_tasks<E, EXACT>(eng, A, scales, order, chunk_tab, n_chunk, weight, stack, (int64_t)xcd_block() * kFft + wave,
@@ -1225,10 +1208,8 @@ template <class E>
 static int64_t table_bytes(int64_t n_pass) {
   return n_pass * (tab_pass_f2<E::kTabBins>() * (int64_t)sizeof(float2) + 2 * kTabEnt * (int64_t)sizeof(int32_t));
 }
-// the stack workspace: the pivot-slice table, then 8 per-XCD task counters of the validated launch
-constexpr int64_t kXcdQBytes = 64;
 static int64_t stack_ws_bytes(int n, int64_t n_pass) {
-  return (n == 500 ? table_bytes<EngF500>(n_pass) : table_bytes<EngP1024>(n_pass)) + kXcdQBytes;
+  return n == 500 ? table_bytes<EngF500>(n_pass) : table_bytes<EngP1024>(n_pass);
 }
 
 static int launch_table(VsgArgs& A, int n, float2* tab, hipStream_t s) {
@@ -1273,15 +1254,12 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   float2* tab = (table_engine(n) && spec_ws) ? reinterpret_cast<float2*>(spec_ws) : nullptr;
   hipError_t e = hipMemsetAsync(work, 0, sizeof(uint32_t) * ((size_t)S.n_win + 2), s);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
-  static const bool xcd_env = !getenv("DVH_VSTACK_XCDQ") || atoi(getenv("DVH_VSTACK_XCDQ")) != 0;  // A/B
-  uint32_t* xq = (tab && xcd_env) ? reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(spec_ws) +
-                                                                stack_ws_bytes(n, n_pass) - kXcdQBytes)
-                                  : nullptr;
-  if (xq && (e = hipMemsetAsync(xq, 0, kXcdQBytes, s)) != hipSuccess) return set_error(-3, hipGetErrorString(e));
-  // the covered-span scan: the fused engines (w = 500, padded 1 024), default windows, 16-byte aligned rows (the
-  // kernel also needs the chunks to list every pass, and falls back to the whole-window scan otherwise)
-  static const int span_env = getenv("DVH_SCAN_SPAN") ? atoi(getenv("DVH_SCAN_SPAN")) : 0;  // A/B
-  int32_t span = (span_env && (n == 500 || n == 1024) && !scan_tab && n_t % 4 == 0 && ch_stride % 4 == 0 && pass_stride % 4 == 0 &&
+  // the covered-span scan: w = 500's fused engine, default windows, 16-byte aligned rows (the kernel also needs the
+  // chunks to list every pass, and falls back to the whole-window scan otherwise).  synth10k launch 13.27-13.28 ->
+  // 13.08-13.13 ms, weights 1.304-1.312 -> 1.278-1.289 ms; on the padded engine it lost (w = 499 synth10k 15.0 ->
+  // 16.8-17.1 ms: its 8 loads per lane in flight against the whole-window scan's 32).  DVH_SCAN_SPAN=0: off (A/B).
+  static const int span_env = getenv("DVH_SCAN_SPAN") ? atoi(getenv("DVH_SCAN_SPAN")) : 1;
+  int32_t span = (span_env && n == 500 && !scan_tab && n_t % 4 == 0 && ch_stride % 4 == 0 && pass_stride % 4 == 0 &&
                   reinterpret_cast<uintptr_t>(win) % 16 == 0 &&
                   ((int64_t)(n_ch - 1) * ch_stride + n_t) * 4 < 0xfffffff0LL) ? 1 : 0;
   if (tab)
@@ -1291,8 +1269,7 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   if (get_vstack(n, &v)) {
     const int64_t need = (tasks + v.fft - 1) / v.fft;
     const int grid = (int)(need < v.bpc * cu_count() ? (need > 0 ? need : 1) : v.bpc * cu_count());
-    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &tab, &xq,
-                    &span};
+    void* args[] = {&A, &scales, &order, &chunk_tab, &n_chunk, &weight, &stack, (void*)&S, &vflag, &counter, &tab, &span};
     if (int rc = launch(v.fn, grid, v.fft + v.scan, v.lds, args, s)) return rc;
     if (span && S.n_win > 0) {  // the windows the covered-span scan could not decide, rescanned whole
       hipLaunchKernelGGL(window_fixup_kernel, dim3((unsigned)S.n_win), dim3(256), 0, s, A, S, vflag);

@@ -100,7 +100,8 @@ int dvh_vsg_stack(const float* win, int64_t pass_stride, int64_t ch_stride, int3
  * window by ||data||_F (preprocessing_window, apis/virtual_shot_gather.py:125), so a NaN / inf
  * anywhere in a window [n_ch][n_t], or an all-zero window, makes that pass's gather -- and the mean of
  * its class -- NaN.  This entry reads every sample of every pass's window once, alongside the
- * correlations, and sets stack[slot] to NaN for each slot (< n_slot) holding such a pass; the
+ * correlations (at w = 500 the validity scan leaves out the samples the correlations load, which check them
+ * themselves), and sets stack[slot] to NaN for each slot (< n_slot) holding such a pass; the
  * scales must then come from dvh_vsg_scales WITHOUT win_sumsq.  Requires flags & (norm | norm_amp):
  * with neither, the scale itself is 1 / ||data||_F^2 (use dvh_window_sumsq).
  * Scan windows: with scan_tab == NULL window p is pass p (win + p * pass_stride, n_ch rows); a unit
@@ -119,9 +120,8 @@ int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64_t ch_st
 /* Bytes of the spec_ws workspace dvh_vsg_stack / dvh_vsg_stack_validated take for n_pass passes at
  * window length w: the spectra of every pass's pivot slices that many rows share (w = 500: the shared
  * windows of both sides and the far rows' clamped windows, 24 KiB + 32 B per pass), which lets the
- * stack launch transform only receivers for those rows (EngF500::spectra_tab), and 64 bytes of per-XCD task
- * counters for dvh_vsg_stack_validated.  0 when w does not use it; with spec_ws == NULL the stack entries run the
- * per-sub-window engine instead. */
+ * stack launch transform only receivers for those rows (EngF500::spectra_tab).  0 when w does not use
+ * it; with spec_ws == NULL the stack entries run the per-sub-window engine instead. */
 int64_t dvh_vsg_stack_workspace(int32_t n_pass, int32_t w);
 
 /* ---------------------------------------------------------------- dispersion (map_fv)
