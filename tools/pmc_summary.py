@@ -19,7 +19,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("vsg_stackv_kernel", "vsg_stackf_kernel", "window_scan_kernel", "vsg_invalid_fill_kernel", "vsg_stack_kernel", "vsg_scales_kernel", "window_sumsq_kernel", "pass_geometry_kernel", "tdft_gemm_kernel", "tdft_rows_kernel", "fk_contract_kernel",
+KERNELS = ("vsg_stackv_kernel", "window_fixup_kernel", "vsg_stackf_kernel", "window_scan_kernel", "vsg_invalid_fill_kernel", "vsg_stack_kernel", "vsg_scales_kernel", "window_sumsq_kernel", "pass_geometry_kernel", "tdft_gemm_kernel", "tdft_rows_kernel", "fk_contract_kernel",
            "fv_kernel", "fv_batch_kernel", "fv_tile_kernel", "fv_mfma_kernel", "vsg_stackp_kernel", "vsg_gather_kernel",
            "sos_block_kernel", "sos_scan_kernel", "sos_transition_kernel", "row_stats_kernel", "impute_kernel",
            "row_normalize_kernel", "select_mean_kernel", "ridge_kernel", "read4", "read16", "atomic4")
