@@ -838,6 +838,9 @@ __device__ __forceinline__ SpanRow span_row(const VsgArgs& A, int p, int row0, i
   return r;
 }
 // rows [c0, c1) of pass p's window (n_t % 4 == 0, 16-byte aligned rows): max |x| bit pattern over the wave
+// D: loads per lane in flight (the kernel's registers are sized for its correlation waves: EngF500's 128 VGPRs take
+// 8, 16 spills; EngP1024 takes 16, 32 spills)
+template <int D>
 __device__ __forceinline__ uint32_t scan_rows_span(const VsgArgs& A, const ScanArgs& S, int p, int c0, int c1, int lane) {
   const float* base = A.win + (int64_t)p * A.pass_stride;
   const int64_t wbytes = ((int64_t)(S.n_ch - 1) * A.ch_stride + S.n_t) * 4;  // < 0xfffffff0 (host)
@@ -859,7 +862,6 @@ __device__ __forceinline__ uint32_t scan_rows_span(const VsgArgs& A, const ScanA
     o += o >= cur.s1 ? cur.d1 : 0;
     return v < cur.U ? cur.base + (uint32_t)o * 16u : kOut;
   };
-  constexpr int D = 8;  // loads per lane in flight (16 spills: the kernel's registers are sized for the correlation)
   uint32_t m = 0;
   u32x4 r[D];
 #pragma unroll
@@ -899,8 +901,8 @@ __global__ __launch_bounds__(256) void window_fixup_kernel(VsgArgs A, ScanArgs S
 }
 
 // Pull scan units (window, kScanRows channel rows) until none is left; atomicMax into vflag[window].  span: the
-// covered-span scan (default windows of a launch whose chunks list every pass).
-template <int D = kScanDepth>
+// covered-span scan (default windows of a launch whose chunks list every pass), DS loads per lane in flight.
+template <int D = kScanDepth, int DS = 8>
 __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, uint32_t* __restrict__ vflag,
                                            uint32_t* __restrict__ counter, int lane,
                                            const int32_t* __restrict__ sorder = nullptr, bool span = false) {
@@ -914,7 +916,7 @@ __device__ __forceinline__ void scan_units(const VsgArgs& A, const ScanArgs& S, 
     const int q = u / upp, c0 = (u - q * upp) * kScanRows;
     const int s = (sorder && !S.tab) ? sld(sorder + q) : q;
     const float* base = S.tab ? A.win + (int64_t)sld(S.tab + s) * A.ch_stride : A.win + (int64_t)s * A.pass_stride;
-    const uint32_t m = span ? scan_rows_span(A, S, s, c0, min(c0 + kScanRows, S.n_ch), lane)
+    const uint32_t m = span ? scan_rows_span<DS>(A, S, s, c0, min(c0 + kScanRows, S.n_ch), lane)
                             : scan_rows<D>(base, A.ch_stride, c0, min(c0 + kScanRows, S.n_ch), S.n_t, vec, lane);
     if (lane == 0) atomicMax(vflag + s, m);
     u = un;
@@ -938,7 +940,7 @@ __device__ __forceinline__ void stack_tasks(E& eng, const VsgArgs& A, const floa
 
 // Persistent validated stack launch: blocks of kFft correlation waves + kScan scan waves (EngF500: two per CU;
 // the 1 024-point engines' LDS and registers allow one).
-template <class E, int kFft, int kScan, int kOcc, bool EXACT = true, int kDepth = kScanDepth>
+template <class E, int kFft, int kScan, int kOcc, bool EXACT = true, int kDepth = kScanDepth, int kSpanDepth = 8>
 __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
     VsgArgs A, const float* __restrict__ scales, const int32_t* __restrict__ order,
     const int32_t* __restrict__ chunk_tab, int32_t n_chunk, const float* __restrict__ weight,
@@ -968,7 +970,7 @@ __global__ __launch_bounds__(64 * (kFft + kScan), kOcc) void vsg_stackv_kernel(
                           src);
     __builtin_amdgcn_s_setprio(0);
   }
-  scan_units<kDepth>(A, S, vflag, counter, lane, sorder, span);
+  scan_units<kDepth, kSpanDepth>(A, S, vflag, counter, lane, sorder, span);
 }
 
 // The validity scan alone (correlation engines without a validated stack kernel).
@@ -1188,15 +1190,16 @@ struct VStack {
   int fft, scan, bpc;
   size_t lds;
 };
-template <class E, int F, int SC, int OCC, bool EXACT, int DEPTH = kScanDepth>
+template <class E, int F, int SC, int OCC, bool EXACT, int DEPTH = kScanDepth, int SPAN = 8>
 static VStack vstack(int bpc) {
-  return VStack{(const void*)vsg_stackv_kernel<E, F, SC, OCC, EXACT, DEPTH>, F, SC, bpc, E::kBlockBytes + F * E::kWaveBytes};
+  return VStack{(const void*)vsg_stackv_kernel<E, F, SC, OCC, EXACT, DEPTH, SPAN>, F, SC, bpc,
+                E::kBlockBytes + F * E::kWaveBytes};
 }
 static bool get_vstack(int n, VStack* v) {
   switch (n) {
     case 500: *v = vstack<EngF500, kVsFft, kVsScan, kVsOcc, true>(kVsBpc); return true;
     case 512: *v = vstack<EngStockham<512, true>, 7, 1, 2, false>(1); return true;
-    case 1024: *v = vstack<EngP1024, kP1Fft, kP1Scan, 2, false, kP1Depth>(1); return true;
+    case 1024: *v = vstack<EngP1024, kP1Fft, kP1Scan, 2, false, kP1Depth, 16>(1); return true;
     default: return false;
   }
 }
@@ -1259,7 +1262,7 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   // 13.08-13.13 ms, weights 1.304-1.312 -> 1.278-1.289 ms; on the padded engine it lost (w = 499 synth10k 15.0 ->
   // 16.8-17.1 ms: its 8 loads per lane in flight against the whole-window scan's 32).  DVH_SCAN_SPAN=0: off (A/B).
   static const int span_env = getenv("DVH_SCAN_SPAN") ? atoi(getenv("DVH_SCAN_SPAN")) : 1;
-  int32_t span = (span_env && n == 500 && !scan_tab && n_t % 4 == 0 && ch_stride % 4 == 0 && pass_stride % 4 == 0 &&
+  int32_t span = (span_env && (n == 500 || (n == 1024 && span_env > 1)) && !scan_tab && n_t % 4 == 0 && ch_stride % 4 == 0 && pass_stride % 4 == 0 &&
                   reinterpret_cast<uintptr_t>(win) % 16 == 0 &&
                   ((int64_t)(n_ch - 1) * ch_stride + n_t) * 4 < 0xfffffff0LL) ? 1 : 0;
   if (tab)
