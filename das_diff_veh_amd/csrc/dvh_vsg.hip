@@ -1181,6 +1181,9 @@ static int cu_count() {
 // registers sized for it by the launch bounds).  EngP1024: 7 + 1 waves, one block per CU (LDS, registers), its scan
 // waves keeping 32 loads per lane in flight (w = 499 synth10k launch 14.70 vs 15.08 ms at 16, 14.92 at 48).
 constexpr int kVsFft = 7, kVsScan = 1, kVsBpc = 2, kVsOcc = 4;
+#ifndef DVH_SPAN_F500
+#define DVH_SPAN_F500 8  // A/B: the covered-span scan's loads per lane in flight in the EngF500 launch (<= 11 spill-free)
+#endif
 constexpr int kP1Fft = 7, kP1Scan = 1, kP1Depth = 32;
 
 // The fused (correlation + validity scan) launch of each transform length: kernel, correlation / scan waves per
@@ -1197,7 +1200,7 @@ static VStack vstack(int bpc) {
 }
 static bool get_vstack(int n, VStack* v) {
   switch (n) {
-    case 500: *v = vstack<EngF500, kVsFft, kVsScan, kVsOcc, true>(kVsBpc); return true;
+    case 500: *v = vstack<EngF500, kVsFft, kVsScan, kVsOcc, true, kScanDepth, DVH_SPAN_F500>(kVsBpc); return true;
     case 512: *v = vstack<EngStockham<512, true>, 7, 1, 2, false>(1); return true;
     case 1024: *v = vstack<EngP1024, kP1Fft, kP1Scan, 2, false, kP1Depth, 16>(1); return true;
     default: return false;

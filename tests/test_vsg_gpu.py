@@ -124,11 +124,15 @@ def test_stack_modes(device, fixture, kw, special):
 
 
 @pytest.mark.parametrize("fixture", ["vsg_w500", "vsg_w499"])
-@pytest.mark.parametrize("kind", ["zero", "nan", "inf", "nan_outside_rows", "inf_in_slice", "nan_in_slice"])
+@pytest.mark.parametrize("kind", ["zero", "nan", "inf", "nan_outside_rows", "inf_in_slice", "nan_in_slice",
+                                  "nan_direct", "nan_zero_pivot"])
 def test_validated_stack_invalid_windows(device, kind, fixture):
     """vsg_stack_validated: an all-zero window, or a NaN / inf anywhere in it (also in channels no gather
     row reads), makes its class mean NaN (data / ||data||_F, apis/virtual_shot_gather.py:125); the
-    other class is unaffected and equals the oracle."""
+    other class is unaffected and equals the oracle.  The slice cases put the sample where the covered-span scan
+    leaves it to the correlation: a trajectory row's slice (P + i R transforms), a one-sided row below the pivot
+    (its receivers packed across passes: the task's non-finite sum sends its passes to the whole-window rescan),
+    and the same with the pivot's slices zeroed (a sub-window never transformed, checked where it is loaded)."""
     import torch
 
     from das_diff_veh_amd.apis.data_classes import SurfaceWaveWindow
@@ -154,20 +158,25 @@ def test_validated_stack_invalid_windows(device, kind, fixture):
         w0 = SurfaceWaveWindow(**a)
         geo = pass_geometry(a["x_axis"], a["t_axis"], w0.veh_state_x, w0.veh_state_t,
                             VsgParams(include_other_side=True, norm=False, **KW))
-        i = geo.pivot_idx - geo.start_idx + 3
+        below = kind in ("nan_direct", "nan_zero_pivot")
+        i = geo.pivot_idx - geo.start_idx + (-3 if below else 3)
         t0, L = geo.seg[i, 0]
         assert L == geo.nsamp and L > 400  # a full-length slice (nsamp = 1000 at w = 500, 999 at w = 499)
         d[geo.start_idx + i, t0 + 400] = np.inf if kind == "inf_in_slice" else np.nan
+        if kind == "nan_zero_pivot":  # the pivot's forward window (the shared slices of the rows below it)
+            tp, Lp = geo.seg[geo.pivot_idx - geo.start_idx, 0]
+            d[geo.pivot_idx, tp:tp + Lp] = 0
     arrs[1]["data"] = d
     wins = [SurfaceWaveWindow(**a) for a in arrs]
-    prm = VsgParams(include_other_side=True, norm=False, **KW)
+    two = kind not in ("nan_direct", "nan_zero_pivot")  # one-sided rows below the pivot: cross-pass packed tasks
+    prm = VsgParams(include_other_side=two, norm=False, **KW)
     (idx, plan), = group_windows(wins, prm, device)[0]
     data = torch.as_tensor(np.stack([w.data for w in wins]), dtype=torch.float32, device=device)
     slots = np.array([i % 2 for i in range(n)])
     got = vsg_stack_validated(data, plan, StackSchedule(slots[idx], 2, chunk=2)).double().cpu().numpy()
     assert plan.w == (500 if fixture == "vsg_w500" else 499)
     assert np.isnan(got[1]).all()
-    refs = [ovsg.virtual_shot_gather(gio.oracle_window(g, i), include_other_side=True, norm=False, **KW)[0]
+    refs = [ovsg.virtual_shot_gather(gio.oracle_window(g, i), include_other_side=two, norm=False, **KW)[0]
             for i in range(n) if slots[i] == 0]
     assert gio.gather_rel_err(got[0], ovsg.stack(refs)) < TOL
 
