@@ -315,9 +315,9 @@ def test_mixed_lag_lengths_bootstrap_and_convergence(device):
     g = gio.load("ridge")
     mode1 = _mode1(g)
     args = ([25, 50], 700, 500, 900, [80, 130], [2.5, 10], [14, 15], [None, mode1])
-    random.seed(3)
+    random.seed(4)  # draws led by w = 500 and by w = 499 passes
     rv, fq = bootstrap_disp(wins, 3, 6, *args)
-    random.seed(3)
+    random.seed(4)
     sels = bt.draw(len(wins), 3, 6)
     assert len({int(bt.GatherCache(wins, **KW).w_of[s[0]]) for s in sels}) == 2  # draws led by both lengths
     fv = bt.GatherCache(wins, **KW).resample_images(sels).cpu().numpy()
@@ -327,6 +327,6 @@ def test_mixed_lag_lengths_bootstrap_and_convergence(device):
             o = orid.extract_ridge_ref_idx(fq[band], bt.VELS, fv[b][:, band], ref_freq_idx=ri - int(np.sum(fq < lb)),
                                            sigma=sg, vel_max=800, ref_vel=vr)
             np.testing.assert_allclose(rv[m][b], o, rtol=0, atol=1e-9)
-    random.seed(4)
+    random.seed(5)
     got = convergence_test(2, wins, 3, *args)
     assert got.shape == (2, 2) and np.all(np.isfinite(got))
