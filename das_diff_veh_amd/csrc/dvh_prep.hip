@@ -369,23 +369,13 @@ __global__ __launch_bounds__(64) void sos_scan_kernel(SosGeom G, const double* _
 // a float64 model of this scheme matches scipy.signal.sosfiltfilt to 1e-13); tests/test_prep_gpu.py holds them to
 // scipy at 1e-10 (float64) / 2e-6 (float32).
 constexpr int kSmL = 64;     // samples per block: four 16-row MFMA tiles
-#ifndef DVH_SOSM_LD
-#define DVH_SOSM_LD 65
-#endif
-#ifndef DVH_SOSM_GA
-#define DVH_SOSM_GA 33
-#endif
-#ifndef DVH_SOSM_OCC
-#define DVH_SOSM_OCC 3
-#endif
-#ifndef DVH_SOSM_SPLIT
-#define DVH_SOSM_SPLIT 0  // A/B: the long dependent MFMA chains (16 k-steps into one accumulator) split over two
-                          // accumulators, per kernel: bit 0 sosm_fa, bit 1 sosm_fc, bit 2 sosm_bc
-#endif
-constexpr int kSmLd = DVH_SOSM_LD;  // LDS image row stride (doubles), odd: the B-operand reads (column li, sample
-                                    // 4 kk + q), which the compiler pairs into ds_read2_b64 (16-lane groups, 32 banks),
-                                    // and the accumulator stores (ds_write_b64, 16-lane groups) of the 16 columns land
-                                    // on 16 distinct bank pairs (at 66 they fell on 8: 2-way conflicts)
+constexpr int kSmLd = 65;  // LDS image row stride (doubles), odd: the B-operand reads (column li, sample 4 kk + q),
+                           // which the compiler pairs into ds_read2_b64 (16-lane groups, 32 banks), and the
+                           // accumulator stores (ds_write_b64, 16-lane groups) of the 16 columns land on 16 distinct
+                           // bank pairs (at 66 they fell on 8: 2-way conflicts; conflict cycles per LDS instruction
+                           // fa / fc / bc 1.73 / 3.44 / 2.51 -> 0.23 / 0.22 / 0.15, profiles/r6_pmc_prep_sosm.json)
+constexpr int kSmOcc = 3;  // sosm_fa / sosm_bc: waves per SIMD the registers are sized for (their LDS allows 3 blocks
+                           // of 4 waves per CU; sosm_fc's 65 KB and 220 registers hold it at 2)
 constexpr int kSmRows = 32;  // state rows of the MFMA tiles (2 NS <= 32)
 typedef double doublex4_t __attribute__((ext_vector_type(4)));
 
@@ -513,7 +503,7 @@ __device__ __forceinline__ double sosm_ext(const T* __restrict__ x, const SosGeo
 //     Toeplitz factors T[i][j] = h[i - j] = hq[q][64 + i - j] and U[i][j] = h[j - i] = hr[q][64 + i - j]
 //   hm[i][m] = Hm[i][m], stride 21;  ga[j][m] = g[L - 1 - j][m], stride 48;  gb[m][i] = g[i][m], stride 66
 //   (rows m >= 2 NS zero)
-constexpr int kHq = 145, kHmLd = 21, kGaLd = DVH_SOSM_GA, kGbLd = DVH_SOSM_LD;
+constexpr int kHq = 145, kHmLd = 21, kGaLd = 33, kGbLd = kSmLd;
 template <int NS>
 __device__ __forceinline__ void sosm_tables(const double* __restrict__ mats, double* hq, double* hr, double* hm, double* ga,
                                             double* gb) {
@@ -693,7 +683,7 @@ __device__ __forceinline__ void sosm_states_out(double* img, int lane, const dou
 
 // Forward phase A: E_f[c] = G u_block for k < nb - 1 (block 0: + M zi u_0, its true end state).
 template <typename T, int NS>
-__global__ __launch_bounds__(256, DVH_SOSM_OCC) void sosm_fa_kernel(const T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
+__global__ __launch_bounds__(256, kSmOcc) void sosm_fa_kernel(const T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
                                                       double* __restrict__ Sf) {
   using O = SosmMats<NS>;
   constexpr int NST = 2 * NS;
@@ -728,20 +718,14 @@ __global__ __launch_bounds__(256, DVH_SOSM_OCC) void sosm_fa_kernel(const T* __r
     if (tile + stride < n_tiles) sosm_fetch_x(x, G, sosm_tile(tile + stride, nr, G.nb), lane, raw);  // next tile
     wave_barrier_lds();
     doublex4_t acc[2] = {doublex4_t{0.0, 0.0, 0.0, 0.0}, doublex4_t{0.0, 0.0, 0.0, 0.0}};
-    doublex4_t acc2[2] = {doublex4_t{0.0, 0.0, 0.0, 0.0}, doublex4_t{0.0, 0.0, 0.0, 0.0}};  // odd k-steps
     const double* bsrc = img + li * kSmLd + q;               // B: sample 4 kk + q of column li
     const double* asrc = ga + q * kGaLd + li;  // A: G[16 t + li][4 kk + q] = ga[4 kk + q][16 t + li]
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const double b = SOSM_B(kk);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        if ((DVH_SOSM_SPLIT & 1) && (kk & 1)) acc2[t] = mfma_f64x4(asrc[4 * kk * kGaLd + 16 * t], b, acc2[t]);
-        else acc[t] = mfma_f64x4(asrc[4 * kk * kGaLd + 16 * t], b, acc[t]);
-      }
+      for (int t = 0; t < 2; ++t) acc[t] = mfma_f64x4(asrc[4 * kk * kGaLd + 16 * t], b, acc[t]);
     }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) acc[t] += acc2[t];
     // block 0 of a row: its true end state M zi u_0 + E (u_0: the column's sample 0, in the image)
     int r, k;
     sosm_col(tl, li, G.nb, r, k);
@@ -842,19 +826,13 @@ __global__ __launch_bounds__(256) void sosm_fc_kernel(const T* __restrict__ x, S
     for (int t = 0; t < 4; ++t) acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
     const double* bsrc = img + li * kSmLd + q;          // B: sample 4 kk + q of column li
     const double* tsrc = hq + q * kHq + kSmL + li - q;  // A: T[16 t + li][4 kk + q] = hq[q][64 + 16 t + li - 4 kk - q]
-    doublex4_t acc2[2] = {doublex4_t{0.0, 0.0, 0.0, 0.0}, doublex4_t{0.0, 0.0, 0.0, 0.0}};  // tiles 2, 3: odd k-steps
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const double b = SOSM_B(kk);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        if (kk <= 4 * t + 3) {  // the lower triangle's k-steps
-          if ((DVH_SOSM_SPLIT & 2) && t >= 2 && (kk & 1)) acc2[t - 2] = mfma_f64x4(tsrc[16 * t - 4 * kk], b, acc2[t - 2]);
-          else acc[t] = mfma_f64x4(tsrc[16 * t - 4 * kk], b, acc[t]);
-        }
+        if (kk <= 4 * t + 3) acc[t] = mfma_f64x4(tsrc[16 * t - 4 * kk], b, acc[t]);  // the lower triangle's k-steps
     }
-#pragma unroll
-    for (int t = 2; t < 4; ++t) acc[t] += acc2[t - 2];
     const double* msrc = hm + li * kHmLd + KS * q;   // A: Hm[16 t + li][KS q + q']
 #pragma unroll
     for (int qq = 0; qq < KS; ++qq)
@@ -863,17 +841,11 @@ __global__ __launch_bounds__(256) void sosm_fc_kernel(const T* __restrict__ x, S
     // backward zero-state end state Gb y: y (rows = samples) as the B operand straight from the accumulators
     // (register rr of tile t is k-step 4 t + rr: sample 16 t + 4 rr + q)
     doublex4_t e[2] = {doublex4_t{0.0, 0.0, 0.0, 0.0}, doublex4_t{0.0, 0.0, 0.0, 0.0}};
-    doublex4_t e2[2] = {doublex4_t{0.0, 0.0, 0.0, 0.0}, doublex4_t{0.0, 0.0, 0.0, 0.0}};  // odd k-steps
     const double* gsrc = gb + li * kGbLd + q;        // A: gb[16 t' + li][4 kk + q]
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        if ((DVH_SOSM_SPLIT & 2) && (kk & 1)) e2[t] = mfma_f64x4(gsrc[16 * t * kGbLd + 4 * kk], acc[kk >> 2][kk & 3], e2[t]);
-        else e[t] = mfma_f64x4(gsrc[16 * t * kGbLd + 4 * kk], acc[kk >> 2][kk & 3], e[t]);
-      }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) e[t] += e2[t];
+      for (int t = 0; t < 2; ++t) e[t] = mfma_f64x4(gsrc[16 * t * kGbLd + 4 * kk], acc[kk >> 2][kk & 3], e[t]);
     // y through the image: coalesced row runs
     wave_barrier_lds();
     sosm_acc_to_lds(img, lane, acc);
@@ -963,7 +935,7 @@ __global__ __launch_bounds__(64) void sosm_bf_kernel(T* __restrict__ x, SosGeom 
 // Backward phase C for backward blocks k' >= 1 (forward blocks k = nb - 1 - k' < nb - 1, columns (r, k) of an
 // [n_rows][nb - 1] grid): v = U y + Hrev s with s the true backward state before the block, trimmed into the row.
 template <typename T, int NS>
-__global__ __launch_bounds__(256, DVH_SOSM_OCC) void sosm_bc_kernel(T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
+__global__ __launch_bounds__(256, kSmOcc) void sosm_bc_kernel(T* __restrict__ x, SosGeom G, const double* __restrict__ mats,
                                                       const double* __restrict__ y, const double* __restrict__ Sb) {
   constexpr int NST = 2 * NS, KS = (NST + 3) / 4;
   __shared__ double hr[4 * kHq], hm[kSmL * kHmLd], imgs[4][16 * kSmLd];
@@ -1010,19 +982,13 @@ __global__ __launch_bounds__(256, DVH_SOSM_OCC) void sosm_bc_kernel(T* __restric
     for (int t = 0; t < 4; ++t) acc[t] = doublex4_t{0.0, 0.0, 0.0, 0.0};
     const double* bsrc = img + li * kSmLd + q;          // B: sample 4 kk + q of column li
     const double* usrc = hr + q * kHq + kSmL + li - q;  // A: U[16 t + li][4 kk + q] = hr[q][64 + 16 t + li - 4 kk - q]
-    doublex4_t acc2[2] = {doublex4_t{0.0, 0.0, 0.0, 0.0}, doublex4_t{0.0, 0.0, 0.0, 0.0}};  // tiles 0, 1: odd k-steps
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const double b = SOSM_B(kk);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        if (kk >= 4 * t) {  // the upper triangle's k-steps
-          if ((DVH_SOSM_SPLIT & 4) && t < 2 && (kk & 1)) acc2[t] = mfma_f64x4(usrc[16 * t - 4 * kk], b, acc2[t]);
-          else acc[t] = mfma_f64x4(usrc[16 * t - 4 * kk], b, acc[t]);
-        }
+        if (kk >= 4 * t) acc[t] = mfma_f64x4(usrc[16 * t - 4 * kk], b, acc[t]);  // the upper triangle's k-steps
     }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) acc[t] += acc2[t];
     const double* msrc = hm + (kSmL - 1 - li) * kHmLd + KS * q;  // A: Hm[L - 1 - (16 t + li)][KS q + q']
 #pragma unroll
     for (int qq = 0; qq < KS; ++qq)

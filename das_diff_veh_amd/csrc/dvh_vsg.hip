@@ -839,7 +839,7 @@ __device__ __forceinline__ SpanRow span_row(const VsgArgs& A, int p, int row0, i
 }
 // rows [c0, c1) of pass p's window (n_t % 4 == 0, 16-byte aligned rows): max |x| bit pattern over the wave
 // D: loads per lane in flight (the kernel's registers are sized for its correlation waves: EngF500's 128 VGPRs take
-// 8, 16 spills; EngP1024 takes 16, 32 spills)
+// 11, 12 spill)
 template <int D>
 __device__ __forceinline__ uint32_t scan_rows_span(const VsgArgs& A, const ScanArgs& S, int p, int c0, int c1, int lane) {
   const float* base = A.win + (int64_t)p * A.pass_stride;
@@ -1181,9 +1181,8 @@ static int cu_count() {
 // registers sized for it by the launch bounds).  EngP1024: 7 + 1 waves, one block per CU (LDS, registers), its scan
 // waves keeping 32 loads per lane in flight (w = 499 synth10k launch 14.70 vs 15.08 ms at 16, 14.92 at 48).
 constexpr int kVsFft = 7, kVsScan = 1, kVsBpc = 2, kVsOcc = 4;
-#ifndef DVH_SPAN_F500
-#define DVH_SPAN_F500 8  // A/B: the covered-span scan's loads per lane in flight in the EngF500 launch (<= 11 spill-free)
-#endif
+constexpr int kVsSpan = 11;  // the covered-span scan's loads per lane in flight in the EngF500 launch: the most without
+                             // spills (12 spill; 11 vs 8: synth10k 13.06 vs 13.09-13.13 ms, profiles/r6_ab)
 constexpr int kP1Fft = 7, kP1Scan = 1, kP1Depth = 32;
 
 // The fused (correlation + validity scan) launch of each transform length: kernel, correlation / scan waves per
@@ -1200,9 +1199,9 @@ static VStack vstack(int bpc) {
 }
 static bool get_vstack(int n, VStack* v) {
   switch (n) {
-    case 500: *v = vstack<EngF500, kVsFft, kVsScan, kVsOcc, true, kScanDepth, DVH_SPAN_F500>(kVsBpc); return true;
+    case 500: *v = vstack<EngF500, kVsFft, kVsScan, kVsOcc, true, kScanDepth, kVsSpan>(kVsBpc); return true;
     case 512: *v = vstack<EngStockham<512, true>, 7, 1, 2, false>(1); return true;
-    case 1024: *v = vstack<EngP1024, kP1Fft, kP1Scan, 2, false, kP1Depth, 16>(1); return true;
+    case 1024: *v = vstack<EngP1024, kP1Fft, kP1Scan, 2, false, kP1Depth>(1); return true;
     default: return false;
   }
 }
@@ -1262,10 +1261,10 @@ DVH_API int dvh_vsg_stack_validated(const float* win, int64_t pass_stride, int64
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
   // the covered-span scan: w = 500's fused engine, default windows, 16-byte aligned rows (the kernel also needs the
   // chunks to list every pass, and falls back to the whole-window scan otherwise).  synth10k launch 13.27-13.28 ->
-  // 13.08-13.13 ms, weights 1.304-1.312 -> 1.278-1.289 ms; on the padded engine it lost (w = 499 synth10k 15.0 ->
-  // 16.8-17.1 ms: its 8 loads per lane in flight against the whole-window scan's 32).  DVH_SCAN_SPAN=0: off (A/B).
+  // 13.06-13.13 ms, weights 1.304-1.312 -> 1.263-1.289 ms; on the padded engine it lost (w = 499 synth10k 14.8-15.0
+  // -> 16.3-17.1 ms at 8 or 16 loads per lane in flight against the whole-window scan's 32).  DVH_SCAN_SPAN=0: off.
   static const int span_env = getenv("DVH_SCAN_SPAN") ? atoi(getenv("DVH_SCAN_SPAN")) : 1;
-  int32_t span = (span_env && (n == 500 || (n == 1024 && span_env > 1)) && !scan_tab && n_t % 4 == 0 && ch_stride % 4 == 0 && pass_stride % 4 == 0 &&
+  int32_t span = (span_env && n == 500 && !scan_tab && n_t % 4 == 0 && ch_stride % 4 == 0 && pass_stride % 4 == 0 &&
                   reinterpret_cast<uintptr_t>(win) % 16 == 0 &&
                   ((int64_t)(n_ch - 1) * ch_stride + n_t) * 4 < 0xfffffff0LL) ? 1 : 0;
   if (tab)
