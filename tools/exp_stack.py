@@ -58,7 +58,8 @@ def main():
     one = UnitScan(np.zeros(1, np.int32), np.zeros(n, np.int32), C)
     # every pass's correlation reads pass 0's window (receivers hot in the caches), the scan still
     # reads every window: isolates what HBM latency under the scan costs the correlation
-    hot = b.win.as_strided((n, C, T), (0, b.win.stride(1), 1))
+    assert b.win.stride(0) == C * b.win.stride(1)
+    hot = b.win.as_strided((n, n * C, T), (0, b.win.stride(1), 1))  # rows span every window for the scan
     allw = UnitScan(np.arange(n, dtype=np.int32) * C, np.arange(n, dtype=np.int32), C)
     out = {}
     fns = {

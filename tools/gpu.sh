@@ -11,7 +11,7 @@
 #   bash tools/gpu.sh pmc TAG [workload]         PMC passes -> profiles/TAG_pmc_summary[_workload].json
 #   bash tools/gpu.sh final TAG                  end of round, first call: tests + smoke, PMC (synth10k, sliding,
 #                                                weights, w = 499, timelapse); the second call is `lines`
-#   bash tools/gpu.sh lines TAG                  every bench line with its CPU baseline (synth10k, weights, sliding,
+#   bash tools/gpu.sh lines TAG [a|b]            every bench line with its CPU baseline (synth10k, weights, sliding,
 #                                                timelapse, w = 499, prep, bootstrap, speeds-host) + kernel stats
 set -o pipefail
 mode=${1:-tests}; shift
@@ -79,19 +79,23 @@ case $mode in
     done
     bash tools/pmc_timelapse.sh $tag > gpurun_out/pmc_tl.log 2>&1 || { echo pmc tl failed; tail -5 gpurun_out/pmc_tl.log; exit 1; }
     rm -rf gpurun_out/pmc_${tag}* ;;
-  lines)
-    tag=$1
-    bench_line gpurun_out/${tag}_bench.json || exit 1
-    bench_line gpurun_out/${tag}_bench_weights.json --workload weights || exit 1
-    bench_line gpurun_out/${tag}_bench_sliding.json --workload sliding --steps 4 --warmup 1 || exit 1
-    bench_line gpurun_out/${tag}_bench_timelapse.json --workload timelapse || exit 1
-    bench_line gpurun_out/${tag}_bench_w499.json --w499 || exit 1
-    bench_line gpurun_out/${tag}_bench_weights_w499.json --workload weights --w499 || exit 1
-    bench_line gpurun_out/${tag}_bench_prep.json --workload prep --steps 20 --warmup 3 || exit 1
-    bench_line gpurun_out/${tag}_bench_bootstrap.json --workload bootstrap --steps 5 --warmup 1 || exit 1
-    bench_line gpurun_out/${tag}_bench_speeds_host.json --workload speeds-host --steps 3 --warmup 1 || exit 1
-    for wl in synth10k weights sliding timelapse prep bootstrap; do bash "$0" prof $tag $wl || exit 1; done
-    bash "$0" profw499 $tag || exit 1 ;;
+  lines)  # part a: the VSG bench lines; part b: the rest + kernel stats (each fits one gpurun call)
+    tag=$1; part=${2:-ab}
+    if [[ $part == *a* ]]; then
+      bench_line gpurun_out/${tag}_bench.json || exit 1
+      bench_line gpurun_out/${tag}_bench_weights.json --workload weights || exit 1
+      bench_line gpurun_out/${tag}_bench_sliding.json --workload sliding --steps 4 --warmup 1 || exit 1
+      bench_line gpurun_out/${tag}_bench_w499.json --w499 || exit 1
+      bench_line gpurun_out/${tag}_bench_weights_w499.json --workload weights --w499 || exit 1
+    fi
+    if [[ $part == *b* ]]; then
+      bench_line gpurun_out/${tag}_bench_timelapse.json --workload timelapse || exit 1
+      bench_line gpurun_out/${tag}_bench_prep.json --workload prep --steps 20 --warmup 3 || exit 1
+      bench_line gpurun_out/${tag}_bench_bootstrap.json --workload bootstrap --steps 5 --warmup 1 || exit 1
+      bench_line gpurun_out/${tag}_bench_speeds_host.json --workload speeds-host --steps 3 --warmup 1 || exit 1
+      for wl in synth10k weights sliding timelapse prep bootstrap; do bash "$0" prof $tag $wl || exit 1; done
+      bash "$0" profw499 $tag || exit 1
+    fi ;;
   profw499)
     tag=$1
     prof_env
