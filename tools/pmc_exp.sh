@@ -6,8 +6,11 @@ tag=$1; only=$2; shift 2
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 d=gpurun_out/pmcx_$tag; rm -rf $d; mkdir -p $d
 i=0
-for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" \
-           "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH"; do
+groups=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU"
+        "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH")
+# PMC_GROUPS="G1;G2": other counter groups (each within one pass's limits)
+[ -n "$PMC_GROUPS" ] && IFS=';' read -ra groups <<< "$PMC_GROUPS"
+for grp in "${groups[@]}"; do
   i=$((i+1))
   env "$@" timeout -s KILL 120 rocprofv3 --pmc $grp -d $d/p$i -o pmc --output-format csv -- python tools/exp_stack.py --reps 3 --only $only $EXP_ARGS > /dev/null 2> $d/p$i.err || { echo "pmc pass $i failed"; tail -3 $d/p$i.err; exit 1; }
 done
