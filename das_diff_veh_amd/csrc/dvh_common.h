@@ -7,4 +7,6 @@
 namespace dvh {
 // Records `msg` as the calling thread's last error and returns `code` (negative).
 int set_error(int code, const char* msg);
+// Compute units of the current device (cached on first use; 256 if the query fails).
+int cu_count();
 }  // namespace dvh

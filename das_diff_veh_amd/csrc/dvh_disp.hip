@@ -110,14 +110,28 @@ __global__ __launch_bounds__(64) void tdft_gemm_kernel(const float* __restrict__
 constexpr int kTdNT = 7;   // 16-column tiles per block (112 columns)
 constexpr int kTdKC = 32;  // k per chunk
 constexpr int kTdRows = 64;
+// Small problems (a few class stacks: configs[1] has 2 x 25 rows, i.e. 5 blocks of the form above, each a chain of
+// 32 chunk round trips, 56 us) split K over G wave groups of one block instead: group g multiplies the chunks
+// kc = g (mod G), the groups' sums are added in group order through LDS (deterministic, no atomics); 2 tiles per
+// block keep the 16-wave block within 128 VGPRs (4 tiles spilled 14).  DVH_TDFT_ROWS=2: never split (A/B).
+constexpr int kTdNTs = 2, kTdGs = 4;
 
-__global__ __launch_bounds__(256) void tdft_rows_kernel(const float* __restrict__ data, int64_t b_stride,
-                                                        int64_t ch_stride, int32_t nch, int32_t M, int32_t K,
-                                                        const double* __restrict__ W, int32_t N,
-                                                        const float* __restrict__ row_scale, double* __restrict__ C) {
-  extern __shared__ __attribute__((aligned(16))) double wsm[];  // [2][kTdKC][kTdNT * 16]
-  constexpr int NC = kTdNT * 16, CH = kTdKC * NC;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+__host__ __device__ constexpr size_t tdft_rows_lds(int NT, int G) {
+  // the groups' staging buffers, or (after the loop) their partial sums, whichever is larger
+  return sizeof(double) * (size_t)G * ((size_t)2 * kTdKC * NT * 16 > (size_t)4 * NT * 4 * 64
+                                           ? (size_t)2 * kTdKC * NT * 16
+                                           : (size_t)4 * NT * 4 * 64);
+}
+
+template <int NT, int G>
+__global__ __launch_bounds__(256 * G) void tdft_rows_kernel(const float* __restrict__ data, int64_t b_stride,
+                                                            int64_t ch_stride, int32_t nch, int32_t M, int32_t K,
+                                                            const double* __restrict__ W, int32_t N,
+                                                            const float* __restrict__ row_scale, double* __restrict__ C) {
+  extern __shared__ __attribute__((aligned(16))) double wsm_all[];  // per group [2][kTdKC][NT * 16]
+  constexpr int NC = NT * 16, CH = kTdKC * NC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) & 3, grp = G > 1 ? (tid >> 8) : 0;
+  double* wsm = wsm_all + (size_t)grp * 2 * CH;
   const int m0 = blockIdx.x * kTdRows + wave * 16, c0 = blockIdx.y * NC;
   const int li = lane & 15, q = lane >> 4;
   const int row = m0 + li;
@@ -126,7 +140,9 @@ __global__ __launch_bounds__(256) void tdft_rows_kernel(const float* __restrict_
   const bool vec4 = ((b_stride | ch_stride) & 3) == 0 && (reinterpret_cast<uintptr_t>(data) & 15) == 0;
   // LDS-DMA of twiddle chunk kc into buffer buf: doubles e = r * NC + c (linear), 2 per lane per piece
   const int n_chunk = (K + kTdKC - 1) / kTdKC;
+  const int n_step = (n_chunk + G - 1) / G;  // every group runs n_step steps (the barriers), idle past n_chunk
   auto stage = [&](int kc, int buf) {
+    if (kc >= n_chunk) return;
     for (int p = wave; p < CH / 128; p += 4) {
       const int e = p * 128 + 2 * lane;
       const int rho = e / NC, c = e - rho * NC;
@@ -148,34 +164,55 @@ __global__ __launch_bounds__(256) void tdft_rows_kernel(const float* __restrict_
       for (int s = 0; s < 8; ++s) a[s] = (rok && kb + s < K) ? (double)rowp[kb + s] : 0.0;
     }
   };
-  doublex4 acc[kTdNT];
+  doublex4 acc[NT];
 #pragma unroll
-  for (int t = 0; t < kTdNT; ++t) acc[t] = doublex4{0.0, 0.0, 0.0, 0.0};
+  for (int t = 0; t < NT; ++t) acc[t] = doublex4{0.0, 0.0, 0.0, 0.0};
   double a[8];
-  stage(0, 0);
-  load_a(0, a);
-  for (int kc = 0; kc < n_chunk; ++kc) {
+  stage(grp, 0);
+  load_a(grp, a);
+  for (int st = 0; st < n_step; ++st) {
+    const int kc = grp + G * st, kn = kc + G;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this chunk's twiddles have landed (and a)
     __syncthreads();  // ... for every wave; the other buffer's last readers are done
     double an[8];
-    if (kc + 1 < n_chunk) {
-      stage(kc + 1, (kc + 1) & 1);
-      load_a(kc + 1, an);
+    if (kn < n_chunk) {
+      stage(kn, (st + 1) & 1);
+      load_a(kn, an);
     }
-    // rows beyond K in a partial chunk multiply a = 0 with finite (clamped) twiddles
-    const double* Wc = wsm + (kc & 1) * CH;
+    if (kc < n_chunk) {
+      // rows beyond K in a partial chunk multiply a = 0 with finite (clamped) twiddles
+      const double* Wc = wsm + (st & 1) * CH;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < 8; ++s) {
 #pragma unroll
-      for (int t = 0; t < kTdNT; ++t) acc[t] = mfma_f64(a[s], Wc[(4 * s + q) * NC + t * 16 + li], acc[t]);
+        for (int t = 0; t < NT; ++t) acc[t] = mfma_f64(a[s], Wc[(4 * s + q) * NC + t * 16 + li], acc[t]);
+      }
     }
-    if (kc + 1 < n_chunk) {
+    if (kn < n_chunk) {
 #pragma unroll
       for (int s = 0; s < 8; ++s) a[s] = an[s];
     }
   }
+  if constexpr (G > 1) {  // group sums in group order: red[g][wave][t][r][lane]
+    __syncthreads();       // every group's last chunk is read
+    double* red = wsm_all;
+    if (grp > 0) {
 #pragma unroll
-  for (int t = 0; t < kTdNT; ++t) {
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(((size_t)grp * 4 + wave) * NT + t) * 256 + r * 64 + lane] = acc[t][r];
+    }
+    __syncthreads();
+    if (grp > 0) return;
+#pragma unroll
+    for (int g = 1; g < G; ++g)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][r] += red[(((size_t)g * 4 + wave) * NT + t) * 256 + r * 64 + lane];
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
     const int col = c0 + t * 16 + li;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1036,13 +1073,18 @@ DVH_API int dvh_disp_tdft(const float* data, int64_t b_stride, int64_t ch_stride
   if (M <= 0 || N <= 0) return 0;
   static const int rows_env = getenv("DVH_TDFT_ROWS") ? atoi(getenv("DVH_TDFT_ROWS")) : 1;
   if (rows_env && (reinterpret_cast<uintptr_t>(wt) & 15) == 0) {  // N = 2 n_fb is even: 16-byte twiddle pieces
-    const size_t lds = sizeof(double) * 2 * kTdKC * kTdNT * 16;
-    hipError_t e = hipFuncSetAttribute((const void*)tdft_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const int64_t blocks = (int64_t)((M + kTdRows - 1) / kTdRows) * ((N + kTdNT * 16 - 1) / (kTdNT * 16));
+    // fewer blocks than a quarter of the CUs: the K-split form (5 -> 8 blocks of 16 waves for configs[1]'s class stacks)
+    const bool split = blocks * 4 < cu_count() && rows_env != 2;
+    const void* fn = split ? (const void*)tdft_rows_kernel<kTdNTs, kTdGs> : (const void*)tdft_rows_kernel<kTdNT, 1>;
+    const int NT = split ? kTdNTs : kTdNT, G = split ? kTdGs : 1;
+    const size_t lds = tdft_rows_lds(NT, G);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));
-    dim3 grid((M + kTdRows - 1) / kTdRows, (N + kTdNT * 16 - 1) / (kTdNT * 16));
-    hipLaunchKernelGGL(tdft_rows_kernel, grid, dim3(256), lds, (hipStream_t)stream, data, b_stride, ch_stride, nch, M,
-                       nt, wt, N, row_scale, D);
-    return last_launch();
+    dim3 grid((M + kTdRows - 1) / kTdRows, (N + NT * 16 - 1) / (NT * 16));
+    void* args[] = {(void*)&data, &b_stride, &ch_stride, &nch, (void*)&M, &nt, (void*)&wt, (void*)&N, (void*)&row_scale, &D};
+    e = hipLaunchKernel(fn, grid, dim3(256 * G), args, lds, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : set_error(-3, hipGetErrorString(e));
   }
   hipError_t e = hipMemsetAsync(D, 0, sizeof(double) * (size_t)M * N, (hipStream_t)stream);
   if (e != hipSuccess) return set_error(-3, hipGetErrorString(e));

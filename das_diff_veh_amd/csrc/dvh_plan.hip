@@ -17,6 +17,8 @@
 // np.argmax(t >= v) on an ascending t is the first index with t[i] >= v, and 0 when none (v above
 // the axis, or NaN).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "dvh_common.h"
@@ -101,7 +103,7 @@ __device__ __forceinline__ int2 py_slice(int64_t a, int64_t b, int64_t n) {
 }
 
 // One block per pass: every thread evaluates f(pivot) (a handful of loads, identical result) and
-// then the rows i = tid, tid + kGeomBlock, ...
+// then the rows i = tid, tid + blockDim.x, ...
 __global__ __launch_bounds__(kGeomBlock) void pass_geometry_kernel(
     const double* __restrict__ x_axis, int64_t x_stride, const double* __restrict__ t_axis, int64_t t_stride,
     int32_t n_t, const double* __restrict__ trk_x, const double* __restrict__ trk_t, int64_t trk_stride,
@@ -165,7 +167,9 @@ DVH_API int dvh_pass_geometry(const double* x_axis, int64_t x_stride, const doub
   if (n_pass < 0 || R <= 0 || n_t < 1 || nsamp < 0 || x_stride < 0 || t_stride < 0 || trk_stride < 0)
     return set_error(-2, "invalid geometry (n_pass, R, n_t, nsamp, strides)");
   if (n_pass == 0) return 0;
-  hipLaunchKernelGGL(pass_geometry_kernel, dim3(n_pass), dim3(kGeomBlock), 0, (hipStream_t)stream, x_axis, x_stride,
+  // one thread per row (whole waves): a narrow gather (configs[1]: R = 49) gets one wave per pass, not 16 idle ones
+  const int block = std::min(kGeomBlock, std::max(64, (R + 63) / 64 * 64));
+  hipLaunchKernelGGL(pass_geometry_kernel, dim3(n_pass), dim3(block), 0, (hipStream_t)stream, x_axis, x_stride,
                      t_axis, t_stride, n_t, trk_x, trk_t, trk_stride, trk_len, pivot_x, pass_tab, R, delta_t, nsamp,
                      flags, seg_tab, status);
   const hipError_t e = hipGetLastError();

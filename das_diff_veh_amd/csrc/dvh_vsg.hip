@@ -656,23 +656,43 @@ __global__ __launch_bounds__(256) void vsg_pivot_table_kernel(VsgArgs A, float2*
     auto pick = [](int e, int a0, int a1, int a2, int a3) { return e == 0 ? a0 : e == 1 ? a1 : e == 2 ? a2 : a3; };
     if (lane < 2 * kTabEnt)
       head[(int64_t)p * 2 * kTabEnt + lane] = (lane & 1) ? pick(lane >> 1, nw0, nw1, nw2, nw3) : pick(lane >> 1, st0, st1, st2, st3);
-    // the slices (e, q), q < kTabSub, two per transform; absent ones are zero
+    // the slices (e, q), q < kTabSub, two per transform; absent ones are zero.  The next pair's samples are loaded
+    // before this pair's transform (one load latency per pass instead of one per transform)
+    constexpr int NL = (N + 63) / 64;
+    auto load_pair = [&](int s0, float (&v0)[NL], float (&v1)[NL], bool& h0, bool& h1) {
+      const int e0 = s0 / kTabSub, q0 = s0 % kTabSub, e1 = (s0 + 1) / kTabSub, q1 = (s0 + 1) % kTabSub;
+      h0 = q0 < pick(e0, nw0, nw1, nw2, nw3);
+      h1 = q1 < pick(e1, nw0, nw1, nw2, nw3);
+      const float* x0 = tp.piv + pick(e0, st0, st1, st2, st3) + q0 * A.hop;
+      const float* x1 = tp.piv + pick(e1, st0, st1, st2, st3) + q1 * A.hop;
+#pragma unroll
+      for (int k = 0; k < NL; ++k) {
+        const int n = lane + 64 * k;
+        const bool in = n < A.w;  // the padded engines' zeros past the sub-window (and n < N, as A.w <= N)
+        v0[k] = (h0 && in) ? x0[n] : 0.f;
+        v1[k] = (h1 && in) ? x1[n] : 0.f;
+      }
+    };
+    float c0[NL], c1[NL];
+    bool ch0, ch1;
+    load_pair(0, c0, c1, ch0, ch1);
 #pragma unroll 1
     for (int s0 = 0; s0 < kTabSub * kTabEnt; s0 += 2) {
       const int e0 = s0 / kTabSub, q0 = s0 % kTabSub, e1 = (s0 + 1) / kTabSub, q1 = (s0 + 1) % kTabSub;
-      const bool h0 = q0 < pick(e0, nw0, nw1, nw2, nw3), h1 = q1 < pick(e1, nw0, nw1, nw2, nw3);
-      const float* x0 = tp.piv + pick(e0, st0, st1, st2, st3) + q0 * A.hop;
-      const float* x1 = tp.piv + pick(e1, st0, st1, st2, st3) + q1 * A.hop;
+      const bool h0 = ch0, h1 = ch1;
       uint32_t nz0 = 0, nz1 = 0;
       const float2* X = nullptr;
       if (h0 || h1) {
-        for (int n = lane; n < N; n += 64) {
-          const bool in = n < A.w;  // the padded engines' zeros past the sub-window
-          const float v0 = (h0 && in) ? x0[n] : 0.f, v1 = (h1 && in) ? x1[n] : 0.f;
-          nz0 |= nzbits(v0);
-          nz1 |= nzbits(v1);
-          bufA[n] = make_float2(v0, v1);
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+          const int n = lane + 64 * k;
+          nz0 |= nzbits(c0[k]);
+          nz1 |= nzbits(c1[k]);
+          if (n < N) bufA[n] = make_float2(c0[k], c1[k]);
         }
+      }
+      if (s0 + 2 < kTabSub * kTabEnt) load_pair(s0 + 2, c0, c1, ch0, ch1);
+      if (h0 || h1) {
         wave_sync();
         X = FftPlan<N>::T::run(bufA, bufB, tw, lane);
       }
@@ -1164,17 +1184,6 @@ DVH_API int dvh_vsg_gathers(const float* win, int64_t pass_stride, int64_t ch_st
   const int64_t grid = (tasks + k.waves - 1) / k.waves;
   void* args[] = {&A, &scales, &out};
   return launch(k.gather, (int)(grid > (1 << 30) ? (1 << 30) : grid), k.waves, k.lds, args, (hipStream_t)stream);
-}
-
-static int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      n = v;
-    if (n <= 0) n = 256;
-  }
-  return n;
 }
 
 // Validated launch shapes.  EngF500: blocks of 7 correlation + 1 scan waves, 2 blocks per CU (4 waves per SIMD, the
