@@ -110,8 +110,8 @@ __global__ __launch_bounds__(64) void tdft_gemm_kernel(const float* __restrict__
 constexpr int kTdNT = 7;   // 16-column tiles per block (112 columns)
 constexpr int kTdKC = 32;  // k per chunk
 constexpr int kTdRows = 64;
-// Small problems (a few class stacks: configs[1] has 2 x 25 rows, i.e. 5 blocks of the form above, each a chain of
-// 32 chunk round trips, 56 us) split K over G wave groups of one block instead: group g multiplies the chunks
+// Small problems (a few class stacks: configs[1]'s six class images make a handful of blocks of the form above, each
+// a chain of 32 chunk round trips, 56 us) split K over G wave groups of one block instead: group g multiplies the chunks
 // kc = g (mod G), the groups' sums are added in group order through LDS (deterministic, no atomics); 2 tiles per
 // block keep the 16-wave block within 128 VGPRs (4 tiles spilled 14).  DVH_TDFT_ROWS=2: never split (A/B).
 constexpr int kTdNTs = 2, kTdGs = 4;
@@ -1074,7 +1074,7 @@ DVH_API int dvh_disp_tdft(const float* data, int64_t b_stride, int64_t ch_stride
   static const int rows_env = getenv("DVH_TDFT_ROWS") ? atoi(getenv("DVH_TDFT_ROWS")) : 1;
   if (rows_env && (reinterpret_cast<uintptr_t>(wt) & 15) == 0) {  // N = 2 n_fb is even: 16-byte twiddle pieces
     const int64_t blocks = (int64_t)((M + kTdRows - 1) / kTdRows) * ((N + kTdNT * 16 - 1) / (kTdNT * 16));
-    // fewer blocks than a quarter of the CUs: the K-split form (5 -> 8 blocks of 16 waves for configs[1]'s class stacks)
+    // fewer blocks than a quarter of the CUs: the K-split form (16 waves per block)
     const bool split = blocks * 4 < cu_count() && rows_env != 2;
     const void* fn = split ? (const void*)tdft_rows_kernel<kTdNTs, kTdGs> : (const void*)tdft_rows_kernel<kTdNT, 1>;
     const int NT = split ? kTdNTs : kTdNT, G = split ? kTdGs : 1;

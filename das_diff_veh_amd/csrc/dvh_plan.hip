@@ -167,7 +167,7 @@ DVH_API int dvh_pass_geometry(const double* x_axis, int64_t x_stride, const doub
   if (n_pass < 0 || R <= 0 || n_t < 1 || nsamp < 0 || x_stride < 0 || t_stride < 0 || trk_stride < 0)
     return set_error(-2, "invalid geometry (n_pass, R, n_t, nsamp, strides)");
   if (n_pass == 0) return 0;
-  // one thread per row (whole waves): a narrow gather (configs[1]: R = 49) gets one wave per pass, not 16 idle ones
+  // one thread per row (whole waves): a narrow gather (configs[1]: R = 48) gets one wave per pass, not 16 idle ones
   const int block = std::min(kGeomBlock, std::max(64, (R + 63) / 64 * 64));
   hipLaunchKernelGGL(pass_geometry_kernel, dim3(n_pass), dim3(block), 0, (hipStream_t)stream, x_axis, x_stride,
                      t_axis, t_stride, n_t, trk_x, trk_t, trk_stride, trk_len, pivot_x, pass_tab, R, delta_t, nsamp,
