@@ -40,6 +40,7 @@ SIGNATURES = {
                           _p, _p, _p, _p, _p],
     "dvh_disp_fv_mfma": [_p, _i32, _i32, _i32, _p, _p, _i32, _i32, _p, _p, _i32, _i32, _p, _p],
     "dvh_select_mean": [_p, _i64, _i64, _p, _i32, _i32, _p, _i64, _p],
+    "dvh_select_mean_var": [_p, _i64, _i64, _p, _p, _p, _i32, _p, _i64, _p],
     "dvh_ridge": [_p, _i64, _i32, _i32, _i32, _i32, _i32, _p, _i32, _f64, _f64, _p, _p, _i32, _p, _p, _p, _p],
     "dvh_sosfiltfilt_workspace": [_i64, _i32, _i32, _i32],
     "dvh_sosfiltfilt": [_p, _i32, _i64, _i64, _i32, _p, _i32, _i32, _p, _p, _p],

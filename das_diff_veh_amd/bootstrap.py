@@ -247,11 +247,9 @@ class GatherCache:
 
     def resample_stacks_sizes(self, sels, start_x=-150, end_x=0, out=None):
         """resample_stacks of several draw sets (sels: list of [B_k, k] arrays, e.g. one per bootstrap size) into
-        consecutive rows of one [sum B_k, nch, w] buffer: every selection crosses to the device in ONE
-        asynchronous copy (device.upload) and each set is one select_mean launch on it, so the host never waits
-        between them."""
-        import ctypes
-
+        consecutive rows of one [sum B_k, nch, w] buffer: every selection, with each resample's offset and size,
+        crosses to the device in ONE asynchronous copy (device.upload) and all resamples are one
+        dvh_select_mean_var launch (60 launches of 30 resamples each were latency-bound: 0.94 ms)."""
         from .device import upload
         sels = [np.asarray(x, dtype=np.int32) for x in sels]
         if not sels or any(x.ndim != 2 or x.size == 0 for x in sels):
@@ -267,15 +265,12 @@ class GatherCache:
             out = torch.empty((B, e + 1 - s, w), dtype=torch.float32, device=self.device)
         elif tuple(out.shape) != (B, e + 1 - s, w) or out.dtype != torch.float32 or not out.is_contiguous():
             raise ValueError(f"out must be a contiguous float32 [{B}, {e + 1 - s}, {w}] tensor")
-        (sel_t,) = upload([flat], self.device)
+        cnt = np.concatenate([np.full(x.shape[0], x.shape[1], dtype=np.int32) for x in sels])
+        off = np.concatenate([[0], np.cumsum(cnt[:-1], dtype=np.int64)]).astype(np.int32)
+        sel_t, off_t, cnt_t = upload([flat, off, cnt], self.device)
         base = self.G[:, s:e + 1, :]
-        off = b0 = 0
-        for x in sels:
-            Bk, k = x.shape
-            _lib.call("dvh_select_mean", _lib.ptr(base), R * w, rows, ctypes.c_void_p(sel_t.data_ptr() + 4 * off), Bk,
-                      k, ctypes.c_void_p(out.data_ptr() + 4 * b0 * rows), rows, _lib.stream_of(self.device))
-            off += x.size
-            b0 += Bk
+        _lib.call("dvh_select_mean_var", _lib.ptr(base), R * w, rows, _lib.ptr(sel_t), _lib.ptr(off_t), _lib.ptr(cnt_t),
+                  B, _lib.ptr(out), rows, _lib.stream_of(self.device))
         return out
 
     def resample_images(self, sel, start_x=-150, end_x=0):

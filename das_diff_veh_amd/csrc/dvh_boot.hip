@@ -18,19 +18,29 @@
 namespace dvh {
 
 // out[b][k] = (sum_{j < m} G[sel[b][j]][k]) / m over the contiguous K-element block of each pass,
-// summed in selection order (the reference's sum(images) / len(images)).  float4 per lane.
-__global__ __launch_bounds__(256) void select_mean_kernel(const float* __restrict__ G, int64_t pass_stride, int64_t K,
-                                                          const int32_t* __restrict__ sel, int32_t m,
-                                                          float* __restrict__ out, int64_t out_stride) {
-  const int b = blockIdx.y;
-  const int32_t* s = sel + (int64_t)b * m;
-  const bool vec = (K % 4 == 0) && (pass_stride % 4 == 0) && (out_stride % 4 == 0) &&
-                   ((reinterpret_cast<uintptr_t>(G) | reinterpret_cast<uintptr_t>(out)) % 16 == 0);
+// summed in selection order (the reference's sum(images) / len(images)).  float4 per lane; the loads of 8
+// selections are issued before their adds (in order), so a lane keeps 8 gathers' reads in flight.
+__device__ __forceinline__ void select_mean_one(const float* __restrict__ G, int64_t pass_stride, int64_t K,
+                                                const int32_t* __restrict__ s, int32_t m, float* __restrict__ o,
+                                                bool vec) {
   if (vec) {
     const int64_t k4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (4 * k4 >= K) return;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int j = 0; j < m; ++j) {
+    int j = 0;
+    for (; j + 8 <= m; j += 8) {
+      float4 g[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) g[u] = reinterpret_cast<const float4*>(G + (int64_t)s[j + u] * pass_stride)[k4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc.x += g[u].x;
+        acc.y += g[u].y;
+        acc.z += g[u].z;
+        acc.w += g[u].w;
+      }
+    }
+    for (; j < m; ++j) {
       const float4 g = reinterpret_cast<const float4*>(G + (int64_t)s[j] * pass_stride)[k4];
       acc.x += g.x;
       acc.y += g.y;
@@ -38,15 +48,40 @@ __global__ __launch_bounds__(256) void select_mean_kernel(const float* __restric
       acc.w += g.w;
     }
     // divide (not multiply by 1/m): sum / len as the reference evaluates it
-    reinterpret_cast<float4*>(out + (int64_t)b * out_stride)[k4] =
-        make_float4(acc.x / (float)m, acc.y / (float)m, acc.z / (float)m, acc.w / (float)m);
+    reinterpret_cast<float4*>(o)[k4] = make_float4(acc.x / (float)m, acc.y / (float)m, acc.z / (float)m, acc.w / (float)m);
   } else {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += (int64_t)gridDim.x * blockDim.x) {
       float acc = 0.f;
       for (int j = 0; j < m; ++j) acc += G[(int64_t)s[j] * pass_stride + k];
-      out[(int64_t)b * out_stride + k] = acc / (float)m;
+      o[k] = acc / (float)m;
     }
   }
+}
+
+__device__ __forceinline__ bool select_vec(const float* G, int64_t pass_stride, int64_t K, const float* out,
+                                           int64_t out_stride) {
+  return (K % 4 == 0) && (pass_stride % 4 == 0) && (out_stride % 4 == 0) &&
+         ((reinterpret_cast<uintptr_t>(G) | reinterpret_cast<uintptr_t>(out)) % 16 == 0);
+}
+
+__global__ __launch_bounds__(256) void select_mean_kernel(const float* __restrict__ G, int64_t pass_stride, int64_t K,
+                                                          const int32_t* __restrict__ sel, int32_t m,
+                                                          float* __restrict__ out, int64_t out_stride) {
+  const int b = blockIdx.y;
+  select_mean_one(G, pass_stride, K, sel + (int64_t)b * m, m, out + (int64_t)b * out_stride, select_vec(G, pass_stride,
+                  K, out, out_stride));
+}
+
+// The same for resamples of different sizes in one launch: resample b takes cnt[b] selections from sel + off[b]
+// (convergence_test's bt_size = 1 .. 60 x 30 draws: one launch of 1 800 resamples instead of 60 of 30).
+__global__ __launch_bounds__(256) void select_mean_var_kernel(const float* __restrict__ G, int64_t pass_stride,
+                                                              int64_t K, const int32_t* __restrict__ sel,
+                                                              const int32_t* __restrict__ off,
+                                                              const int32_t* __restrict__ cnt, float* __restrict__ out,
+                                                              int64_t out_stride) {
+  const int b = blockIdx.y;
+  select_mean_one(G, pass_stride, K, sel + off[b], cnt[b], out + (int64_t)b * out_stride,
+                  select_vec(G, pass_stride, K, out, out_stride));
 }
 
 // np.argmax order over (value, row): a NaN beats any number, the first row wins ties
@@ -241,6 +276,18 @@ DVH_API int dvh_select_mean(const float* G, int64_t pass_stride, int64_t K, cons
   const int64_t blocks = (K / 4 + 255) / 256 + 1;
   hipLaunchKernelGGL(select_mean_kernel, dim3((unsigned)blocks, B), dim3(256), 0, (hipStream_t)stream, G, pass_stride,
                      K, sel, m, out, out_stride);
+  return last_launch();
+}
+
+DVH_API int dvh_select_mean_var(const float* G, int64_t pass_stride, int64_t K, const int32_t* sel, const int32_t* off,
+                                const int32_t* cnt, int32_t B, float* out, int64_t out_stride, void* stream) {
+  if (!G || !sel || !off || !cnt || !out) return set_error(-2, "null pointer argument");
+  if (K < 0 || B < 0) return set_error(-2, "invalid sizes");
+  if (B == 0 || K == 0) return 0;
+  if (B > 65535) return set_error(-4, "too many resamples for one launch");
+  const int64_t blocks = (K / 4 + 255) / 256 + 1;
+  hipLaunchKernelGGL(select_mean_var_kernel, dim3((unsigned)blocks, B), dim3(256), 0, (hipStream_t)stream, G,
+                     pass_stride, K, sel, off, cnt, out, out_stride);
   return last_launch();
 }
 

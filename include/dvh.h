@@ -184,6 +184,11 @@ int dvh_disp_fv_mfma(const double* FK, int32_t B, int32_t n_kb, int32_t n_fb, co
 int dvh_select_mean(const float* G, int64_t pass_stride, int64_t K, const int32_t* sel, int32_t B, int32_t m,
                     float* out, int64_t out_stride, void* stream);
 
+/* dvh_select_mean for resamples of different sizes in one launch: resample b averages the cnt[b] >= 1 passes
+ * sel[off[b] .. off[b] + cnt[b]) (device arrays; convergence_test's bt_size = 1 .. max_size draws). */
+int dvh_select_mean_var(const float* G, int64_t pass_stride, int64_t K, const int32_t* sel, const int32_t* off,
+                        const int32_t* cnt, int32_t B, float* out, int64_t out_stride, void* stream);
+
 /* extract_ridge_ref_idx on the frequency band [c0, c0 + nb) of fv[b] ([nV][nF], b_stride elements
  * apart), rows = velocities vel[nV] strictly descending.  ref == INT32_MIN: vel_max mode (raw picks
  * below argmin |vel_max - vel|); vref (nullable, [nb]): per-frequency reference velocities; otherwise

@@ -93,18 +93,29 @@ def test_resample_stacks_and_images(device):
 
 
 def test_resample_stacks_sizes_equal_per_size(device):
-    """resample_stacks_sizes (convergence's one upload + one select_mean launch per size) equals resample_stacks
-    called per size, row for row, including sizes of one pass and repeated passes."""
+    """resample_stacks_sizes (convergence's one upload + one dvh_select_mean_var launch) equals resample_stacks
+    called per size, row for row, including sizes of one pass, repeated passes and sizes past the kernel's 8-load
+    groups, and a float32 sum in selection order divided by the size (sum(images) / len(images)), bit for bit."""
     import torch
 
     from das_diff_veh_amd import bootstrap as bt
     wins, _ = _windows()
     cache = bt.GatherCache(wins, **KW)
     rng = np.random.default_rng(5)
-    sels = [rng.integers(0, cache.n, size=(3, k)).astype(np.int32) for k in (1, 2, 4, 3)]
+    sels = [rng.integers(0, cache.n, size=(3, k)).astype(np.int32) for k in (1, 2, 4, 3, 8, 9, 17)]
     got = cache.resample_stacks_sizes(sels)
     want = torch.cat([cache.resample_stacks(x) for x in sels])
     assert torch.equal(got, want)
+    s_, e_, _ = cache.disp_plan()
+    G = cache.G[:, s_:e_ + 1, :].cpu().numpy()
+    ref = []
+    for x in sels:
+        for row in x:
+            acc = np.zeros(G.shape[1:], np.float32)
+            for j in row:
+                acc += G[j]
+            ref.append(acc / np.float32(len(row)))
+    assert np.array_equal(got.cpu().numpy(), np.stack(ref))
     with pytest.raises(ValueError):
         cache.resample_stacks_sizes([np.array([[0, cache.n]], np.int32)])
 
