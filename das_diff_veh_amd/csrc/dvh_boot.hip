@@ -126,6 +126,54 @@ __device__ __forceinline__ int first_at_or_below(const double* __restrict__ vel,
   return lo;
 }
 
+// The velocity axis of a walk held in the wave's registers (nV <= 1024: lane l holds rows l S .. l S + S - 1,
+// S = ceil(nV / 64)), so that each step's two window bounds and its pick's velocity cost no memory round trip (the
+// binary searches over vel[] were 2 x 10 dependent loads per step, the walk's critical path).  Same results as
+// first_below / first_at_or_below / vel[r] on a descending axis; larger axes use those.
+struct VelAxis {
+  static constexpr int kMaxS = 16;
+  const double* vel;
+  int nV, S, lane;
+  bool regs;
+  double v[kMaxS];
+  __device__ VelAxis(const double* vel_, int nV_, int lane_) : vel(vel_), nV(nV_), S((nV_ + 63) / 64), lane(lane_) {
+    regs = nV <= 64 * kMaxS;
+#pragma unroll
+    for (int k = 0; k < kMaxS; ++k) {
+      const int r = lane * S + k;
+      v[k] = (regs && k < S && r < nV) ? vel[r] : 0.0;
+    }
+  }
+  // first row whose velocity satisfies the monotone predicate (rows past nV count as satisfying it), nV if none
+  template <class P>
+  __device__ __forceinline__ int first(P pred) const {
+    int f = S;
+#pragma unroll
+    for (int k = 0; k < kMaxS; ++k) {
+      const int r = lane * S + k;
+      if (k < S && f == S && (r >= nV || pred(v[k]))) f = k;
+    }
+    const uint64_t m = __ballot(f < S);
+    if (m == 0) return nV;
+    const int L = __ffsll((unsigned long long)m) - 1;
+    return min(L * S + __shfl(f, L), nV);
+  }
+  __device__ __forceinline__ int below(double x) const {  // first_below
+    return regs ? first([x](double u) { return u < x; }) : first_below(vel, nV, x);
+  }
+  __device__ __forceinline__ int at_or_below(double x) const {  // first_at_or_below
+    return regs ? first([x](double u) { return u <= x; }) : first_at_or_below(vel, nV, x);
+  }
+  __device__ __forceinline__ double at(int r) const {  // vel[r] for a wave-uniform row r
+    if (!regs) return vel[r];
+    const int k = r % S;
+    double u = 0.0;
+#pragma unroll
+    for (int j = 0; j < kMaxS; ++j) u = j == k ? v[j] : u;
+    return __shfl(u, r / S);
+  }
+};
+
 // argmax of column c over rows [r0, r1) (first max wins); -1 when the range is empty
 __device__ __forceinline__ int column_argmax(const float* __restrict__ F, int nF, int c, int r0, int r1, int lane) {
   float best = 0.f;
@@ -191,12 +239,25 @@ __global__ __launch_bounds__(64) void ridge_kernel(const float* __restrict__ fv,
     if (lane == 0) status[b] = err;
     return;
   }
-  if (vref) {
-    for (int i = 0; i < nb; ++i) {
-      const int r0 = first_below(vel, nV, vref[i] + sigma), r1 = first_at_or_below(vel, nV, vref[i] - sigma);
+  const VelAxis ax(vel, nV, lane);
+  // the walk over columns i_begin, i_begin + dir, ... (i_end excluded) from the pick velocity v; returns the last pick
+  auto walk = [&](int i_begin, int i_end, int dir, double v) {
+    for (int i = i_begin; i != i_end; i += dir) {
+      const int r0 = ax.below(v + sigma), r1 = ax.at_or_below(v - sigma);
       const int r = column_argmax(F, nF, c0 + i, r0, r1, lane);
       err |= r < 0;
-      if (lane == 0) pick[i] = r >= 0 ? vel[r] : NAN;
+      v = r >= 0 ? ax.at(r) : NAN;  // (r is wave-uniform: every lane takes part in the shuffle)
+      if (lane == 0) pick[i] = v;
+    }
+    return v;
+  };
+  if (vref) {
+    for (int i = 0; i < nb; ++i) {
+      const int r0 = ax.below(vref[i] + sigma), r1 = ax.at_or_below(vref[i] - sigma);
+      const int r = column_argmax(F, nF, c0 + i, r0, r1, lane);
+      err |= r < 0;
+      const double pv = r >= 0 ? ax.at(r) : NAN;
+      if (lane == 0) pick[i] = pv;
     }
   } else if (ref < 0) {
     // a negative reference index is a Python index: out[ref] is column nb + ref, the backward loop
@@ -204,37 +265,15 @@ __global__ __launch_bounds__(64) void ridge_kernel(const float* __restrict__ fv,
     // nb - 1 and then 0 .. nb - 1 again, seeded by out[-1] (modules/utils.py:662-671)
     const int k0 = nb + ref;
     const int rr = column_argmax(F, nF, c0 + k0, 0, nV, lane);
-    double v = rr >= 0 ? vel[rr] : NAN;
+    const double v = rr >= 0 ? ax.at(rr) : NAN;
     if (lane == 0) pick[k0] = v;
-    for (int pass = 0; pass < 2; ++pass) {
-      for (int i = pass == 0 ? k0 + 1 : 0; i < nb; ++i) {
-        const int r0 = first_below(vel, nV, v + sigma), r1 = first_at_or_below(vel, nV, v - sigma);
-        const int r = column_argmax(F, nF, c0 + i, r0, r1, lane);
-        err |= r < 0;
-        v = r >= 0 ? vel[r] : NAN;
-        if (lane == 0) pick[i] = v;
-      }
-    }
+    walk(0, nb, 1, walk(k0 + 1, nb, 1, v));
   } else {
     const int rr = column_argmax(F, nF, c0 + ref, 0, nV, lane);
-    const double vr = rr >= 0 ? vel[rr] : NAN;  // wave-uniform (every lane holds the reduced row)
-    double v = vr;
-    if (lane == 0) pick[ref] = v;
-    for (int i = ref - 1; i >= 0; --i) {  // backward
-      const int r0 = first_below(vel, nV, v + sigma), r1 = first_at_or_below(vel, nV, v - sigma);
-      const int r = column_argmax(F, nF, c0 + i, r0, r1, lane);
-      err |= r < 0;
-      v = r >= 0 ? vel[r] : NAN;
-      if (lane == 0) pick[i] = v;
-    }
-    v = vr;
-    for (int i = ref + 1; i < nb; ++i) {  // forward
-      const int r0 = first_below(vel, nV, v + sigma), r1 = first_at_or_below(vel, nV, v - sigma);
-      const int r = column_argmax(F, nF, c0 + i, r0, r1, lane);
-      err |= r < 0;
-      v = r >= 0 ? vel[r] : NAN;
-      if (lane == 0) pick[i] = v;
-    }
+    const double vr = rr >= 0 ? ax.at(rr) : NAN;  // wave-uniform (every lane holds the reduced row)
+    if (lane == 0) pick[ref] = vr;
+    walk(ref - 1, -1, -1, vr);  // backward
+    walk(ref + 1, nb, 1, vr);   // forward
   }
   __syncthreads();
   if (picks)  // the raw picks before smoothing (parity checks of each pick)

@@ -57,6 +57,31 @@ def test_ridge_negative_reference_index(device):
         ridges(fv, fq, vels, 2.5, 14, ref_freq_idx=-nb - 1, sigma=25, vel_max=800)
 
 
+@pytest.mark.parametrize("nV", [1000, 63, 65, 1024, 1500])
+def test_ridge_velocity_axis_sizes(device, nV):
+    """The walk's velocity axis in registers (nV <= 1 024: 16 rows per lane at most, ragged last lane) and the
+    global-memory binary search past it: picks (walk, reference-curve and negative-index modes) equal the oracle's
+    extract_ridge_ref_idx on a resampled copy of the golden map."""
+    import torch
+
+    from das_diff_veh_amd.bootstrap import ridges
+    from oracle import ridge as orid
+    g = gio.load("ridge")
+    fq, vels0, fv0 = g["freqs"], g["vels"], g["fv_map"]
+    vels = np.linspace(vels0[0], vels0[-1], nV)  # the golden axis' range and order, nV points
+    fvm = fv0[np.linspace(0, vels0.size - 1, nV).round().astype(int)].astype(np.float32)
+    fv = torch.as_tensor(fvm, device=device)[None]
+    cases = ((2.5, 14, 80 - int(np.sum(fq < 2.5)), 25, None), (2.5, 14, -3, 25, None),
+             (10, 15, 130 - int(np.sum(fq < 10)), 50, _mode1(g)))
+    for lb, ub, ref, sig, rv in cases:
+        m = (fq >= lb) & (fq < ub)
+        got = ridges(fv, fq, vels, lb, ub, ref_freq_idx=ref, sigma=sig, vel_max=800, ref_vel=rv)[0]
+        want = orid.extract_ridge_ref_idx(fq[m], vels, fvm[:, m].astype(np.float64), ref_freq_idx=ref, sigma=sig,
+                                          vel_max=800, ref_vel=rv)
+        assert len(got) == int(m.sum())
+        np.testing.assert_allclose(got, want, rtol=0, atol=1e-9)
+
+
 def test_extract_ridge_mirror(device):
     from das_diff_veh_amd.modules.utils import extract_ridge_ref_idx
     g = gio.load("ridge")
